@@ -1,0 +1,344 @@
+// C ABI of libgraphwalk (include/graphwalk.h): argument validation, error
+// reporting and dispatch to the host builders / HIP entry points.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "gw_internal.h"
+
+// host implementations (gw_graph_host.cpp)
+int gw_load_edgelist_impl(gw_graph* g, const char* path, const char* delim, int semantics,
+                          int directed, int weighted, int64_t vcount);
+int gw_rmat_impl(gw_graph* g, int scale, int edge_factor, double a, double b, double c,
+                 uint64_t seed);
+int gw_write_walks_impl(const gw_graph* g, const char* path, const int32_t* walks,
+                        const int32_t* lens, int64_t nwalks, int walk_len, std::string* err);
+int gw_write_sim_dense_impl(const char* path, const double* rows, const int32_t* row_ids,
+                            int64_t nrows, int64_t n, int topk, const std::string& sep,
+                            int decimals, std::string* err);
+int gw_write_sim_topk_impl(const char* path, const int32_t* ids, const double* scores,
+                           const int32_t* row_ids, int64_t nrows, int topk,
+                           const std::string& sep, int decimals, std::string* err);
+int gw_hip_device_count(int* count);
+
+static thread_local std::string tls_err;
+
+void gw_set_tls_error(const std::string& s) { tls_err = s; }
+
+int gw_fail(gw_graph* g, int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (g) g->err = buf;
+  tls_err = buf;
+  return code;
+}
+
+// propagate a handle error to the thread-local slot too
+static int ret(gw_graph* g, int rc) {
+  if (rc != GW_OK && g) tls_err = g->err;
+  return rc;
+}
+
+extern "C" {
+
+const char* gw_version(void) { return "graphwalk 0.1.0 (gfx950)"; }
+
+const char* gw_last_error(const gw_graph* g) {
+  if (g) return g->err.c_str();
+  return tls_err.c_str();
+}
+
+const char* gw_strerror(int code) {
+  switch (code) {
+    case GW_OK: return "ok";
+    case GW_ERR_INVALID: return "invalid argument";
+    case GW_ERR_IO: return "I/O error";
+    case GW_ERR_PARSE: return "parse error";
+    case GW_ERR_NOMEM: return "out of memory";
+    case GW_ERR_DEVICE: return "HIP device error";
+    case GW_ERR_STATE: return "invalid call order";
+    case GW_ERR_UNSUPPORTED: return "unsupported";
+    case GW_ERR_RANGE: return "id out of range";
+    case GW_ERR_KEY: return "missing key";
+    case GW_ERR_ZERODIV: return "division by zero";
+    case GW_ERR_CAPACITY: return "capacity exceeded";
+    default: return "unknown error";
+  }
+}
+
+int gw_device_count(int* count) {
+  if (!count) return gw_fail(nullptr, GW_ERR_INVALID, "count is NULL");
+  int rc = gw_hip_device_count(count);
+  if (rc != GW_OK) return gw_fail(nullptr, rc, "no HIP device visible");
+  return GW_OK;
+}
+
+int gw_graph_load_edgelist(const char* path, const char* delim, int semantics, int directed,
+                           int weighted, int64_t vcount, gw_graph** out) {
+  if (!path || !out) return gw_fail(nullptr, GW_ERR_INVALID, "path/out is NULL");
+  *out = nullptr;
+  if (semantics == GW_SEM_JAVA_MULTI && (weighted || directed))
+    return gw_fail(nullptr, GW_ERR_UNSUPPORTED, "JAVA_MULTI graphs are undirected and unweighted (Graph.java:12)");
+  gw_graph* g = new gw_graph();
+  int rc = gw_load_edgelist_impl(g, path, delim, semantics, directed, weighted, vcount);
+  if (rc != GW_OK) {
+    tls_err = g->err;
+    delete g;
+    return rc;
+  }
+  *out = g;
+  return GW_OK;
+}
+
+int gw_graph_from_edges(int64_t m, const int64_t* src, const int64_t* dst, const double* w,
+                        int semantics, int directed, int64_t vcount, gw_graph** out) {
+  if (!out || m < 0 || (m > 0 && (!src || !dst))) return gw_fail(nullptr, GW_ERR_INVALID, "bad edge arrays");
+  *out = nullptr;
+  gw_graph* g = new gw_graph();
+  int rc;
+  if (semantics == GW_SEM_NX_SIMPLE)
+    rc = gw_build_nx_simple(g, m, src, dst, w, directed);
+  else if (semantics == GW_SEM_JAVA_MULTI)
+    rc = (w || directed) ? gw_fail(g, GW_ERR_UNSUPPORTED, "JAVA_MULTI graphs are undirected and unweighted")
+                         : gw_build_java_multi(g, m, src, dst, vcount);
+  else
+    rc = gw_fail(g, GW_ERR_INVALID, "unknown semantics %d", semantics);
+  if (rc != GW_OK) {
+    tls_err = g->err;
+    delete g;
+    return rc;
+  }
+  *out = g;
+  return GW_OK;
+}
+
+int gw_graph_from_csr(int64_t n, const int64_t* offsets, const int32_t* nbrs, const double* weights,
+                      const int64_t* labels, const int32_t* node_order, int semantics, int directed,
+                      gw_graph** out) {
+  if (!out || n < 0 || !offsets) return gw_fail(nullptr, GW_ERR_INVALID, "bad CSR arguments");
+  *out = nullptr;
+  if (semantics != GW_SEM_NX_SIMPLE && semantics != GW_SEM_JAVA_MULTI)
+    return gw_fail(nullptr, GW_ERR_INVALID, "unknown semantics %d", semantics);
+  if (n >= (int64_t)INT32_MAX) return gw_fail(nullptr, GW_ERR_UNSUPPORTED, "too many vertices");
+  if (offsets[0] != 0) return gw_fail(nullptr, GW_ERR_INVALID, "offsets[0] != 0");
+  for (int64_t v = 0; v < n; ++v)
+    if (offsets[v + 1] < offsets[v]) return gw_fail(nullptr, GW_ERR_INVALID, "offsets not monotone at %lld", (long long)v);
+  const int64_t nnz = offsets[n];
+  if (nnz > 0 && !nbrs) return gw_fail(nullptr, GW_ERR_INVALID, "nbrs is NULL");
+  for (int64_t v = 0; v < n; ++v)
+    for (int64_t k = offsets[v]; k < offsets[v + 1]; ++k) {
+      if (nbrs[k] < 0 || nbrs[k] >= n) return gw_fail(nullptr, GW_ERR_RANGE, "neighbour id %d out of range", nbrs[k]);
+      if (semantics == GW_SEM_NX_SIMPLE && k > offsets[v] && nbrs[k] <= nbrs[k - 1])
+        return gw_fail(nullptr, GW_ERR_INVALID, "NX_SIMPLE rows must be strictly increasing (row %lld)", (long long)v);
+    }
+  gw_graph* g = new gw_graph();
+  g->semantics = semantics;
+  g->directed = directed ? 1 : 0;
+  g->weighted = weights ? 1 : 0;
+  g->n = n;
+  g->nnz = nnz;
+  g->offsets.assign(offsets, offsets + n + 1);
+  g->nbrs.assign(nbrs, nbrs + nnz);
+  if (weights) g->weights.assign(weights, weights + nnz);
+  g->labels.resize(n);
+  g->order.resize(n);
+  std::vector<char> seen(n, 0);
+  for (int64_t v = 0; v < n; ++v) {
+    g->labels[v] = labels ? labels[v] : v;
+    int32_t o = node_order ? node_order[v] : (int32_t)v;
+    if (o < 0 || o >= n || seen[o]) {
+      delete g;
+      return gw_fail(nullptr, GW_ERR_INVALID, "node_order is not a permutation of [0,n)");
+    }
+    seen[o] = 1;
+    g->order[v] = o;
+  }
+  g->max_degree = 0;
+  for (int64_t v = 0; v < n; ++v) g->max_degree = std::max<int64_t>(g->max_degree, offsets[v + 1] - offsets[v]);
+  *out = g;
+  return GW_OK;
+}
+
+int gw_graph_rmat(int scale, int edge_factor, double a, double b, double c, uint64_t seed,
+                  gw_graph** out) {
+  if (!out) return gw_fail(nullptr, GW_ERR_INVALID, "out is NULL");
+  *out = nullptr;
+  gw_graph* g = new gw_graph();
+  int rc = gw_rmat_impl(g, scale, edge_factor, a, b, c, seed);
+  if (rc != GW_OK) {
+    tls_err = g->err;
+    delete g;
+    return rc;
+  }
+  *out = g;
+  return GW_OK;
+}
+
+int gw_graph_info(const gw_graph* g, gw_graph_info_t* info) {
+  if (!g || !info) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle/info");
+  info->n = g->n;
+  info->nnz = g->nnz;
+  info->max_degree = g->max_degree;
+  info->edge_alias_entries = g->edge_alias_entries;
+  info->semantics = g->semantics;
+  info->directed = g->directed;
+  info->weighted = g->weighted;
+  info->device = g->device;
+  return GW_OK;
+}
+
+int gw_graph_export_csr(const gw_graph* g, int64_t* offsets, int32_t* nbrs, double* weights,
+                        int64_t* labels, int32_t* node_order) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  if (offsets) memcpy(offsets, g->offsets.data(), sizeof(int64_t) * (g->n + 1));
+  if (nbrs && g->nnz) memcpy(nbrs, g->nbrs.data(), sizeof(int32_t) * g->nnz);
+  if (weights && g->nnz) {
+    if (g->weighted)
+      memcpy(weights, g->weights.data(), sizeof(double) * g->nnz);
+    else
+      for (int64_t i = 0; i < g->nnz; ++i) weights[i] = 1.0;
+  }
+  if (labels && g->n) memcpy(labels, g->labels.data(), sizeof(int64_t) * g->n);
+  if (node_order && g->n) memcpy(node_order, g->order.data(), sizeof(int32_t) * g->n);
+  return GW_OK;
+}
+
+int gw_graph_free(gw_graph* g) {
+  if (!g) return GW_OK;
+  gw_dev_release(g);
+  delete g;
+  return GW_OK;
+}
+
+int gw_graph_to_device(gw_graph* g, int device) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  return ret(g, gw_dev_upload(g, device));
+}
+
+int gw_n2v_prepare(gw_graph* g, double p, double q, int mode) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  if (!(p > 0) || !(q > 0)) return ret(g, gw_fail(g, GW_ERR_ZERODIV, "p and q must be > 0 (node2vec.py:70-76 divides by them)"));
+  if (mode != GW_N2V_REPLAY && mode != GW_N2V_REJECTION) return ret(g, gw_fail(g, GW_ERR_INVALID, "unknown mode %d", mode));
+  if (g->semantics != GW_SEM_NX_SIMPLE && !(p == 1.0 && q == 1.0))
+    return ret(g, gw_fail(g, GW_ERR_UNSUPPORTED, "biased walks need NX_SIMPLE semantics (sorted rows)"));
+  if (g->weighted) {
+    for (int64_t v = 0; v < g->n; ++v) {
+      double s = 0;
+      for (int64_t k = g->offsets[v]; k < g->offsets[v + 1]; ++k) s += g->weights[k];
+      if (g->offsets[v + 1] > g->offsets[v] && s == 0.0)
+        return ret(g, gw_fail(g, GW_ERR_ZERODIV, "weights of vertex %lld sum to 0 (node2vec.py:95)", (long long)g->labels[v]));
+    }
+  }
+  return ret(g, gw_dev_n2v_prepare(g, p, q, mode));
+}
+
+int gw_n2v_export_alias(const gw_graph* g_, int32_t* node_J, double* node_q, int64_t* edge_off,
+                        int32_t* edge_J, double* edge_q);
+
+int gw_alias_setup(int device, const double* probs, int64_t K, int64_t* J, double* q) {
+  if (K < 0 || (K > 0 && (!probs || !J || !q))) return gw_fail(nullptr, GW_ERR_INVALID, "bad arrays");
+  std::string err;
+  int rc = gw_dev_alias_setup(device, probs, K, J, q, &err);
+  if (rc != GW_OK) return gw_fail(nullptr, rc, "%s", err.c_str());
+  return GW_OK;
+}
+
+int gw_n2v_walks_replay(gw_graph* g, int walk_len, int64_t nwalks, const int32_t* starts,
+                        const double* uniforms, int64_t n_uniforms, int32_t* out_walks,
+                        int32_t* out_len, int64_t* uniforms_used) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  if (!g->n2v_prepared || g->n2v_mode != GW_N2V_REPLAY)
+    return ret(g, gw_fail(g, GW_ERR_STATE, "call gw_n2v_prepare(..., GW_N2V_REPLAY) first"));
+  if (walk_len < 1 || nwalks < 0 || (nwalks > 0 && (!starts || !out_walks || !out_len)) ||
+      n_uniforms < 0 || (n_uniforms > 0 && !uniforms))
+    return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
+  for (int64_t w = 0; w < nwalks; ++w)
+    if (starts[w] < 0 || starts[w] >= g->n) return ret(g, gw_fail(g, GW_ERR_KEY, "start vertex %d not in graph", starts[w]));
+  if (nwalks == 0) {
+    if (uniforms_used) *uniforms_used = 0;
+    return GW_OK;
+  }
+  return ret(g, gw_dev_n2v_walks_replay(g, walk_len, nwalks, starts, uniforms, n_uniforms, out_walks,
+                                        out_len, uniforms_used));
+}
+
+int gw_n2v_walks(gw_graph* g, int walk_len, uint64_t seed, int64_t walk_begin, int64_t walk_count,
+                 int shuffle, int32_t* out_walks_dev, int32_t* out_len_dev, uint64_t* counters_dev,
+                 void* stream) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  if (!g->n2v_prepared) return ret(g, gw_fail(g, GW_ERR_STATE, "call gw_n2v_prepare first"));
+  if (walk_len < 1 || walk_begin < 0 || walk_count < 0 || (walk_count > 0 && !out_walks_dev))
+    return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
+  if (g->n == 0) return walk_count == 0 ? GW_OK : ret(g, gw_fail(g, GW_ERR_INVALID, "empty graph"));
+  return ret(g, gw_dev_n2v_walks(g, walk_len, seed, walk_begin, walk_count, shuffle, out_walks_dev,
+                                 out_len_dev, counters_dev, stream));
+}
+
+int gw_topsim_prepare(gw_graph* g, int variant, int sample, int step, int topk) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  return ret(g, gw_dev_topsim_prepare(g, variant, sample, step, topk));
+}
+
+int gw_topsim(gw_graph* g, int variant, int sample, int step, double C, uint64_t seed,
+              const int32_t* sources_dev, int64_t nsrc, int topk, int32_t* out_ids_dev,
+              double* out_scores_dev, int64_t* stats_dev, void* stream) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  if (g->device < 0) return ret(g, gw_fail(g, GW_ERR_STATE, "graph is not on a device"));
+  if (nsrc < 0 || (nsrc > 0 && (!sources_dev || !out_ids_dev || !out_scores_dev)) || topk < 0)
+    return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
+  return ret(g, gw_dev_topsim(g, variant, sample, step, C, seed, sources_dev, nsrc, topk, out_ids_dev,
+                              out_scores_dev, nullptr, stats_dev, stream));
+}
+
+int gw_topsim_dense(gw_graph* g, int variant, int sample, int step, double C, uint64_t seed,
+                    const int32_t* sources_dev, int64_t nsrc, double* out_rows_dev,
+                    int64_t* stats_dev, void* stream) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  if (g->device < 0) return ret(g, gw_fail(g, GW_ERR_STATE, "graph is not on a device"));
+  if (nsrc < 0 || (nsrc > 0 && (!sources_dev || !out_rows_dev)))
+    return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
+  return ret(g, gw_dev_topsim(g, variant, sample, step, C, seed, sources_dev, nsrc, 0, nullptr, nullptr,
+                              out_rows_dev, stats_dev, stream));
+}
+
+int gw_write_walks_text(const gw_graph* g, const char* path, const int32_t* walks,
+                        const int32_t* lens, int64_t nwalks, int walk_len) {
+  if (!g || !path || (nwalks > 0 && !walks) || walk_len < 1)
+    return gw_fail(nullptr, GW_ERR_INVALID, "bad arguments");
+  for (int64_t i = 0; i < nwalks * (int64_t)walk_len; ++i)
+    if (walks[i] >= g->n) return gw_fail(nullptr, GW_ERR_RANGE, "walk entry %d outside the graph", walks[i]);
+  std::string err;
+  int rc = gw_write_walks_impl(g, path, walks, lens, nwalks, walk_len, &err);
+  if (rc != GW_OK) return gw_fail(nullptr, rc, "%s", err.c_str());
+  return GW_OK;
+}
+
+int gw_write_sim_text_dense(const char* path, const double* rows, const int32_t* row_ids,
+                            int64_t nrows, int64_t n, int topk, const char* sep, int decimals) {
+  if (!path || (nrows > 0 && !rows) || n < 0 || topk < 0 || decimals < 0 || decimals > 30)
+    return gw_fail(nullptr, GW_ERR_INVALID, "bad arguments");
+  std::string err;
+  int rc = gw_write_sim_dense_impl(path, rows, row_ids, nrows, n, topk, sep ? sep : ",", decimals, &err);
+  if (rc != GW_OK) return gw_fail(nullptr, rc, "%s", err.c_str());
+  return GW_OK;
+}
+
+int gw_write_sim_text_topk(const char* path, const int32_t* ids, const double* scores,
+                           const int32_t* row_ids, int64_t nrows, int topk, const char* sep,
+                           int decimals) {
+  if (!path || (nrows > 0 && (!ids || !scores)) || topk < 0 || decimals < 0 || decimals > 30)
+    return gw_fail(nullptr, GW_ERR_INVALID, "bad arguments");
+  std::string err;
+  int rc = gw_write_sim_topk_impl(path, ids, scores, row_ids, nrows, topk, sep ? sep : ",", decimals, &err);
+  if (rc != GW_OK) return gw_fail(nullptr, rc, "%s", err.c_str());
+  return GW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,69 @@
+// Device-side helpers shared by the HIP translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "gw_internal.h"
+#include "gw_philox.h"
+
+#define GW_HIP_TRY(expr)                                                     \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess) {                                                  \
+      g->err = std::string(#expr) + ": " + hipGetErrorString(_e);            \
+      return GW_ERR_DEVICE;                                                  \
+    }                                                                        \
+  } while (0)
+
+// Binary search for `key` in the sorted row nbrs[b, e); returns the slot or
+// -1.  Rows of NX_SIMPLE graphs are sorted by dense id (== label order), see
+// gw_graph_host.cpp.
+__device__ __forceinline__ int64_t gw_row_find(const int32_t* __restrict__ nbrs,
+                                               int64_t b, int64_t e,
+                                               int32_t key) {
+  int64_t lo = b, hi = e;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (nbrs[mid] < key)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return (lo < e && nbrs[lo] == key) ? lo : -1;
+}
+
+// Sequential Vose/Walker alias construction exactly as node2vec.py:116-147:
+// q[k] = K*p_k; `smaller`/`larger` are LIFO lists filled in index order;
+// J[small] = large; q[large] = (q[large] + q[small]) - 1.0.
+// On entry q[] holds the probabilities; stack[] is K int32 scratch.  J is
+// zero-filled here (np.zeros).  Both stacks share one array: `smaller`
+// grows up from 0, `larger` grows down from K (an index is in at most one
+// stack at a time, so they never collide).
+template <typename JT>
+__device__ __forceinline__ void gw_alias_build(double* q, JT* J, int32_t* stack,
+                                               int64_t K) {
+  const double Kd = (double)K;
+  int64_t s_top = 0, l_top = K;
+  for (int64_t k = 0; k < K; ++k) {
+    J[k] = 0;
+    double v = Kd * q[k];
+    q[k] = v;
+    if (v < 1.0)
+      stack[s_top++] = (int32_t)k;
+    else
+      stack[--l_top] = (int32_t)k;
+  }
+  while (s_top > 0 && l_top < K) {
+    int32_t small = stack[--s_top];
+    int32_t large = stack[l_top++];
+    J[small] = (JT)large;
+    double nv = (q[large] + q[small]) - 1.0;
+    q[large] = nv;
+    if (nv < 1.0)
+      stack[s_top++] = large;
+    else
+      stack[--l_top] = large;
+  }
+}

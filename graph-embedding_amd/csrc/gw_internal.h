@@ -1,0 +1,112 @@
+// Internal definitions shared by the host translation units and the HIP
+// translation units of libgraphwalk.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/graphwalk.h"
+
+// Device-side mirror of the CSR (all pointers are HBM allocations owned by
+// the handle).  Layout (SoA, one array per field so each gather touches only
+// the bytes it needs):
+//   offsets  int64[n+1]   row bounds (16 B per step: offsets[v], offsets[v+1])
+//   nbrs     int32[nnz]   neighbour dense ids, row order = draw order
+//   weights  f64[nnz]     (weighted graphs only)
+//   wsum     f64[n]       per-row weight sums (weighted graphs only)
+//   order    int32[n]     reference G.nodes() order (walk start order)
+//   deg      int32[n]     row lengths (TopSim reads deg(mid), deg(target))
+//   node_J/q int32/f64[nnz] per-node alias tables (weighted or REPLAY)
+//   edge_off int64[nnz+1], edge_J/q per-edge alias tables (REPLAY only)
+struct gw_dev_graph {
+  int64_t n = 0, nnz = 0;
+  int64_t* offsets = nullptr;
+  int32_t* nbrs = nullptr;
+  double* weights = nullptr;
+  double* wsum = nullptr;
+  int32_t* order = nullptr;
+  int32_t* deg = nullptr;
+  int32_t* node_J = nullptr;
+  double* node_q = nullptr;
+  int64_t* edge_off = nullptr;
+  int32_t* edge_J = nullptr;
+  double* edge_q = nullptr;
+};
+
+struct gw_topsim_ws {
+  int variant = -1, sample = 0, step = 0, topk = 0;
+  int blocks = 0;               // persistent workgroups
+  int64_t level_cap = 0;        // records per level per workgroup
+  int64_t spawn_cap = 0;        // spawner records per workgroup
+  int64_t touch_cap = 0;        // distinct targets per workgroup
+  int lds_row = 0;              // accumulator row lives in LDS
+  size_t lds_bytes = 0;         // dynamic LDS per workgroup
+  int32_t* lvl_vertex = nullptr;  // [blocks][levels][level_cap]
+  int32_t* lvl_parent = nullptr;  // [blocks][levels][level_cap]
+  double* lvl_mass = nullptr;     // [blocks][2][level_cap] (current/next)
+  int32_t* child_off = nullptr;   // [blocks][level_cap+1] expansion scan
+  int32_t* spawn_node = nullptr;  // [blocks][spawn_cap] index into its level
+  int32_t* spawn_level = nullptr; // [blocks][spawn_cap]
+  int32_t* spawn_first = nullptr; // [blocks][spawn_cap+1] walker prefix
+  double* spawn_mass = nullptr;   // [blocks][spawn_cap] child mass m/ceil(m)
+  double* acc_row = nullptr;      // [blocks][n] (only when n too big for LDS)
+  int32_t* touched = nullptr;     // [blocks][touch_cap]
+  unsigned int* src_counter = nullptr;  // work queue head
+  int* error_flag = nullptr;      // capacity overflow
+};
+
+struct gw_graph {
+  // host CSR
+  int semantics = 0;
+  int directed = 0;
+  int weighted = 0;
+  int64_t n = 0, nnz = 0, max_degree = 0;
+  std::vector<int64_t> offsets;  // n+1
+  std::vector<int32_t> nbrs;     // nnz
+  std::vector<double> weights;   // nnz (empty if unweighted)
+  std::vector<int64_t> labels;   // n (dense id -> original label)
+  std::vector<int32_t> order;    // n (G.nodes() order as dense ids)
+  // device state
+  int device = -1;
+  gw_dev_graph d;
+  // node2vec state
+  int n2v_prepared = 0;
+  int n2v_mode = -1;
+  double p = 1.0, q = 1.0;
+  int64_t edge_alias_entries = 0;
+  // TopSim state
+  gw_topsim_ws ts;
+  std::string err;
+};
+
+// error helpers (gw_capi.cpp)
+int gw_fail(gw_graph* g, int code, const char* fmt, ...);
+void gw_set_tls_error(const std::string& s);
+
+// host graph builders (gw_graph_host.cpp)
+int gw_build_nx_simple(gw_graph* g, int64_t m, const int64_t* src,
+                       const int64_t* dst, const double* w, int directed);
+int gw_build_java_multi(gw_graph* g, int64_t m, const int64_t* src,
+                        const int64_t* dst, int64_t vcount);
+
+// device code entry points (gw_*.hip), all return GW_* codes
+int gw_dev_upload(gw_graph* g, int device);
+void gw_dev_release(gw_graph* g);
+int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode);
+int gw_dev_alias_setup(int device, const double* probs, int64_t K, int64_t* J,
+                       double* q, std::string* err);
+int gw_dev_n2v_walks_replay(gw_graph* g, int walk_len, int64_t nwalks,
+                            const int32_t* starts, const double* uniforms,
+                            int64_t n_uniforms, int32_t* out_walks,
+                            int32_t* out_len, int64_t* uniforms_used);
+int gw_dev_n2v_walks(gw_graph* g, int walk_len, uint64_t seed,
+                     int64_t walk_begin, int64_t walk_count, int shuffle,
+                     int32_t* out_walks_dev, int32_t* out_len_dev,
+                     uint64_t* counters_dev, void* stream);
+int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step,
+                          int topk);
+int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C,
+                  uint64_t seed, const int32_t* sources_dev, int64_t nsrc,
+                  int topk, int32_t* out_ids_dev, double* out_scores_dev,
+                  double* out_rows_dev, int64_t* stats_dev, void* stream);

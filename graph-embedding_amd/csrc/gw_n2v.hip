@@ -1,0 +1,657 @@
+// node2vec walk generation on gfx950 (H1).
+//
+// Reference: node2vec/src/node2vec.py
+//   preprocess_transition_probs :83-113   -> k_alias_nodes, k_alias_edges
+//   get_alias_edge               :61-81    -> k_alias_edges (bias per dst_nbr)
+//   alias_setup                  :116-147  -> gw_alias_build (device)
+//   alias_draw                   :150-160  -> replay kernel draw
+//   node2vec_walk / simulate_walks :13-59  -> k_walk_replay / k_walk_scale
+//
+// Work decomposition: one lane per walk.  A walk is a dependent chain of
+// gathers (row bounds -> candidate -> [has_edge probe] -> next row), so the
+// kernel is latency/gather bound: occupancy (waves in flight per CU) and
+// bytes per step are the levers, MFMA is irrelevant.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "gw_device_common.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+inline unsigned grid_for(int64_t n, int block = kBlock) {
+  int64_t g = (n + block - 1) / block;
+  return (unsigned)std::max<int64_t>(1, g);
+}
+
+template <typename T>
+int dev_alloc(gw_graph* g, T** p, int64_t count) {
+  *p = nullptr;
+  if (count <= 0) return GW_OK;
+  hipError_t e = hipMalloc((void**)p, sizeof(T) * (size_t)count);
+  if (e != hipSuccess) {
+    g->err = std::string("hipMalloc(") + std::to_string(sizeof(T) * (size_t)count) + " B): " + hipGetErrorString(e);
+    *p = nullptr;
+    return GW_ERR_NOMEM;
+  }
+  return GW_OK;
+}
+
+template <typename T>
+void dev_free(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+// ---------------------------------------------------------------------------
+// preprocessing kernels
+// ---------------------------------------------------------------------------
+__global__ void k_degree_wsum(int64_t n, const int64_t* __restrict__ off,
+                              const double* __restrict__ w, int32_t* __restrict__ deg,
+                              double* __restrict__ wsum) {
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n) return;
+  int64_t b = off[v], e = off[v + 1];
+  deg[v] = (int32_t)(e - b);
+  if (w) {
+    double s = 0.0;  // sequential left-to-right sum, as Python sum()
+    for (int64_t k = b; k < e; ++k) s += w[k];
+    wsum[v] = s;
+  }
+}
+
+// alias_nodes (node2vec.py:91-97): probs = w / sum(w) over the sorted row.
+__global__ void k_alias_nodes(int64_t n, const int64_t* __restrict__ off,
+                              const double* __restrict__ w, int32_t* __restrict__ J,
+                              double* __restrict__ q, int32_t* __restrict__ stack) {
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n) return;
+  int64_t b = off[v], e = off[v + 1];
+  int64_t K = e - b;
+  if (K == 0) return;
+  double norm = 0.0;
+  if (w) {
+    for (int64_t k = b; k < e; ++k) norm += w[k];
+  } else {
+    norm = (double)K;  // sum of int 1 weights (main.py:84-85)
+  }
+  for (int64_t k = 0; k < K; ++k) q[b + k] = (w ? w[b + k] : 1.0) / norm;
+  gw_alias_build<int32_t>(q + b, J + b, stack + b, K);
+}
+
+// per-slot table sizes for alias_edges: size(e) = deg(nbrs[e])
+__global__ void k_edge_sizes(int64_t nnz, const int32_t* __restrict__ nbrs,
+                             const int32_t* __restrict__ deg, int64_t* __restrict__ sz) {
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nnz) return;
+  sz[e] = deg[nbrs[e]];
+}
+
+// alias_edges (node2vec.py:61-81, :102-108): for slot e = (src -> dst), the
+// table over sorted N(dst): dst_nbr == src -> w/p ; elif has_edge(dst_nbr,
+// src) -> w ; else w/q ; normalised by the sequential sum.
+__global__ void k_alias_edges(int64_t n, int64_t nnz, const int64_t* __restrict__ off,
+                              const int32_t* __restrict__ nbrs, const double* __restrict__ w,
+                              double p, double q, const int64_t* __restrict__ eoff,
+                              int32_t* __restrict__ eJ, double* __restrict__ eq,
+                              int32_t* __restrict__ stack) {
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nnz) return;
+  // src = row containing slot e (upper_bound over offsets)
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (off[mid + 1] <= e)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  const int32_t src = (int32_t)lo;
+  const int32_t dst = nbrs[e];
+  const int64_t db = off[dst], de = off[dst + 1];
+  const int64_t K = de - db;
+  if (K == 0) return;
+  double* qt = eq + eoff[e];
+  double norm = 0.0;
+  for (int64_t k = 0; k < K; ++k) {
+    const int32_t x = nbrs[db + k];
+    const double wx = w ? w[db + k] : 1.0;
+    double u;
+    if (x == src) {
+      u = wx / p;
+    } else if (gw_row_find(nbrs, off[x], off[x + 1], src) >= 0) {  // G.has_edge(x, src)
+      u = wx;
+    } else {
+      u = wx / q;
+    }
+    qt[k] = u;
+    norm += u;
+  }
+  for (int64_t k = 0; k < K; ++k) qt[k] = qt[k] / norm;
+  gw_alias_build<int32_t>(qt, eJ + eoff[e], stack + eoff[e], K);
+}
+
+__global__ void k_alias_single(const double* __restrict__ probs, int64_t K,
+                               int64_t* __restrict__ J, double* __restrict__ q,
+                               int32_t* __restrict__ stack) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  for (int64_t k = 0; k < K; ++k) q[k] = probs[k];
+  gw_alias_build<int64_t>(q, J, stack, K);
+}
+
+// ---------------------------------------------------------------------------
+// exact replay walk (node2vec.py:13-39 with alias_draw :150-160)
+// ---------------------------------------------------------------------------
+__global__ void k_walk_replay(gw_dev_graph G, int L, int64_t nwalks,
+                              const int32_t* __restrict__ starts,
+                              const double* __restrict__ U, int64_t nU,
+                              const int64_t* __restrict__ uoff,
+                              int32_t* __restrict__ out, int32_t* __restrict__ lens,
+                              int* __restrict__ overrun) {
+  int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= nwalks) return;
+  int32_t* row = out + w * (int64_t)L;
+  int32_t cur = starts[w];
+  row[0] = cur;
+  int len = 1;
+  int64_t o = uoff[w];
+  int64_t slot = -1;
+  while (len < L) {
+    const int64_t b = G.offsets[cur], e = G.offsets[cur + 1];
+    const int64_t d = e - b;
+    if (d == 0) break;  // directed sink (node2vec.py:36-37)
+    if (o + 2 > nU) {   // caller supplied too few uniforms
+      atomicOr(overrun, 1);
+      break;
+    }
+    const double u1 = U[o], u2 = U[o + 1];
+    o += 2;
+    int64_t kk = (int64_t)floor(u1 * (double)d);  // int(np.floor(rand()*K))
+    if (kk >= d) kk = d - 1;
+    const int32_t* J;
+    const double* q;
+    if (len == 1) {
+      J = G.node_J + b;
+      q = G.node_q + b;
+    } else {
+      const int64_t t0 = G.edge_off[slot];
+      J = G.edge_J + t0;
+      q = G.edge_q + t0;
+    }
+    const int64_t idx = (u2 < q[kk]) ? kk : (int64_t)J[kk];
+    slot = b + idx;
+    cur = G.nbrs[slot];
+    row[len++] = cur;
+  }
+  for (int t = len; t < L; ++t) row[t] = -1;
+  lens[w] = len;
+}
+
+// ---------------------------------------------------------------------------
+// scale walk: Philox4x32-10, per-node alias (weighted) or uniform
+// (unweighted) proposal, exact second-order bias by rejection with the return
+// edge as an outlier (KnightKing-style envelope).
+// ---------------------------------------------------------------------------
+struct N2VParams {
+  double a_p, a_q;   // 1/p, 1/q
+  double M;          // envelope height for non-return candidates = max(1, 1/q)
+  double lo;         // min(1, 1/q): accept without probing below this
+  double extra;      // outlier height for the return edge = max(0, 1/p - M)
+  double h_prev;     // min(1/p, M): in-envelope height of the return edge
+  uint32_t k0, k1;   // step key
+  uint32_t pk0, pk1; // permutation key
+};
+
+template <bool WEIGHTED>
+__device__ __forceinline__ int64_t draw_first_order(const gw_dev_graph& G, int64_t b,
+                                                    int64_t d, uint32_t ux, uint32_t uy) {
+  int64_t kk = (int64_t)gw_bounded(ux, (uint32_t)d);
+  if (!WEIGHTED) return kk;
+  return (gw_u01(uy) < G.node_q[b + kk]) ? kk : (int64_t)G.node_J[b + kk];
+}
+
+template <bool FIRST_ORDER, bool WEIGHTED, bool DIRECTED>
+__global__ void __launch_bounds__(kBlock)
+k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_count,
+             int shuffle, int32_t* __restrict__ out, int32_t* __restrict__ lens,
+             unsigned long long* __restrict__ counters) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long my_steps = 0, my_trials = 0;
+  if (i < walk_count) {
+    const int64_t w = walk_begin + i;
+    const uint64_t it = (uint64_t)w / (uint64_t)G.n;
+    const uint64_t pos = (uint64_t)w % (uint64_t)G.n;
+    const uint64_t sp = shuffle ? gw_feistel_perm(pos, (uint64_t)G.n, P.pk0, P.pk1, (uint32_t)it) : pos;
+    int32_t cur = G.order[sp];
+    int32_t prev = -1;
+    int64_t pb = 0, pe = 0;  // prev row bounds (undirected has_edge probes)
+    double w_back = 1.0;     // weight of edge cur<->prev (outlier area)
+    bool back_ok = false;    // cur -> prev exists (always true undirected)
+    int32_t* row = out + i * (int64_t)L;
+    row[0] = cur;
+    int len = 1;
+    const uint32_t c0 = (uint32_t)w, c1 = (uint32_t)((uint64_t)w >> 32);
+    while (len < L) {
+      const int64_t b = G.offsets[cur], e = G.offsets[cur + 1];
+      const int64_t d = e - b;
+      if (d == 0) break;
+      int64_t slot;
+      int32_t next;
+      if (FIRST_ORDER || len == 1) {
+        gw_u4 u = gw_philox(c0, c1, (uint32_t)len, 0u, P.k0, P.k1);
+        ++my_trials;
+        slot = b + draw_first_order<WEIGHTED>(G, b, d, u.x, u.y);
+        next = G.nbrs[slot];
+      } else {
+        double Wcur = WEIGHTED ? G.wsum[cur] : (double)d;
+        double out_area = (back_ok && P.extra > 0.0) ? P.extra * w_back : 0.0;
+        double A = P.M * Wcur + out_area;
+        uint32_t trial = 0;
+        for (;;) {
+          gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
+          ++trial;
+          if (out_area > 0.0 && gw_u01(u.z) * A < out_area) {  // return-edge outlier
+            slot = -1;
+            next = prev;
+            break;
+          }
+          const int64_t s = b + draw_first_order<WEIGHTED>(G, b, d, u.x, u.y);
+          const int32_t x = G.nbrs[s];
+          const double t = gw_u01(u.w) * P.M;
+          bool acc;
+          if (x == prev) {
+            acc = t < P.h_prev;
+          } else if (t < P.lo) {
+            acc = true;
+          } else {
+            bool adj;
+            if (DIRECTED)
+              adj = gw_row_find(G.nbrs, G.offsets[x], G.offsets[x + 1], prev) >= 0;  // edge x -> prev
+            else
+              adj = gw_row_find(G.nbrs, pb, pe, x) >= 0;  // x in N(prev)
+            acc = t < (adj ? 1.0 : P.a_q);
+          }
+          if (acc || trial >= (1u << 24)) {
+            slot = s;
+            next = x;
+            break;
+          }
+        }
+        my_trials += trial;
+      }
+      // carry state for the next step: existence/weight of edge next -> cur
+      if (DIRECTED) {
+        if (!FIRST_ORDER && P.extra > 0.0) {  // probe once per step
+          const int64_t bs = gw_row_find(G.nbrs, G.offsets[next], G.offsets[next + 1], cur);
+          back_ok = bs >= 0;
+          w_back = (back_ok && WEIGHTED) ? G.weights[bs] : 1.0;
+        }
+      } else if (slot >= 0) {
+        back_ok = true;
+        w_back = WEIGHTED ? G.weights[slot] : 1.0;
+      }  // undirected return over the same edge: w_back unchanged
+      prev = cur;
+      pb = b;
+      pe = e;
+      cur = next;
+      row[len++] = cur;
+    }
+    for (int t = len; t < L; ++t) row[t] = -1;
+    if (lens) lens[i] = len;
+    my_steps = (unsigned long long)(len - 1);
+  }
+  if (counters) {
+    // wave-level reduction, one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) {
+      my_steps += __shfl_down(my_steps, off, 64);
+      my_trials += __shfl_down(my_trials, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&counters[0], my_steps);
+      atomicAdd(&counters[1], my_trials);
+    }
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// host entry points
+// ---------------------------------------------------------------------------
+void gw_dev_release(gw_graph* g) {
+  if (g->device < 0) return;
+  (void)hipSetDevice(g->device);
+  gw_dev_graph& d = g->d;
+  dev_free(d.offsets);
+  dev_free(d.nbrs);
+  dev_free(d.weights);
+  dev_free(d.wsum);
+  dev_free(d.order);
+  dev_free(d.deg);
+  dev_free(d.node_J);
+  dev_free(d.node_q);
+  dev_free(d.edge_off);
+  dev_free(d.edge_J);
+  dev_free(d.edge_q);
+  gw_topsim_ws& t = g->ts;
+  dev_free(t.lvl_vertex);
+  dev_free(t.lvl_parent);
+  dev_free(t.lvl_mass);
+  dev_free(t.child_off);
+  dev_free(t.spawn_node);
+  dev_free(t.spawn_mass);
+  dev_free(t.spawn_level);
+  dev_free(t.spawn_first);
+  dev_free(t.acc_row);
+  dev_free(t.touched);
+  dev_free(t.src_counter);
+  dev_free(t.error_flag);
+  t = gw_topsim_ws();
+  g->n2v_prepared = 0;
+  g->device = -1;
+}
+
+int gw_dev_upload(gw_graph* g, int device) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+    g->err = "no HIP device visible (libgraphwalk has no CPU fallback)";
+    return GW_ERR_DEVICE;
+  }
+  if (device < 0 || device >= count) {
+    g->err = "device ordinal out of range";
+    return GW_ERR_INVALID;
+  }
+  if (g->device >= 0) gw_dev_release(g);
+  GW_HIP_TRY(hipSetDevice(device));
+  g->device = device;
+  gw_dev_graph& d = g->d;
+  d.n = g->n;
+  d.nnz = g->nnz;
+  int rc;
+  if ((rc = dev_alloc(g, &d.offsets, g->n + 1)) || (rc = dev_alloc(g, &d.nbrs, g->nnz)) ||
+      (rc = dev_alloc(g, &d.order, g->n)) || (rc = dev_alloc(g, &d.deg, g->n))) {
+    gw_dev_release(g);
+    return rc;
+  }
+  GW_HIP_TRY(hipMemcpy(d.offsets, g->offsets.data(), sizeof(int64_t) * (g->n + 1), hipMemcpyHostToDevice));
+  if (g->nnz) GW_HIP_TRY(hipMemcpy(d.nbrs, g->nbrs.data(), sizeof(int32_t) * g->nnz, hipMemcpyHostToDevice));
+  if (g->n) GW_HIP_TRY(hipMemcpy(d.order, g->order.data(), sizeof(int32_t) * g->n, hipMemcpyHostToDevice));
+  if (g->weighted) {
+    if ((rc = dev_alloc(g, &d.weights, g->nnz)) || (rc = dev_alloc(g, &d.wsum, g->n))) {
+      gw_dev_release(g);
+      return rc;
+    }
+    if (g->nnz) GW_HIP_TRY(hipMemcpy(d.weights, g->weights.data(), sizeof(double) * g->nnz, hipMemcpyHostToDevice));
+  }
+  if (g->n) {
+    k_degree_wsum<<<grid_for(g->n), kBlock>>>(g->n, d.offsets, d.weights, d.deg, d.wsum);
+    GW_HIP_TRY(hipGetLastError());
+  }
+  GW_HIP_TRY(hipDeviceSynchronize());
+  return GW_OK;
+}
+
+int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
+  if (g->device < 0) {
+    g->err = "graph is not on a device (call gw_graph_to_device)";
+    return GW_ERR_STATE;
+  }
+  GW_HIP_TRY(hipSetDevice(g->device));
+  gw_dev_graph& d = g->d;
+  dev_free(d.node_J);
+  dev_free(d.node_q);
+  dev_free(d.edge_off);
+  dev_free(d.edge_J);
+  dev_free(d.edge_q);
+  g->edge_alias_entries = 0;
+  g->n2v_prepared = 0;
+  const bool need_node_alias = g->weighted || mode == GW_N2V_REPLAY;
+  int rc;
+  int32_t* stack = nullptr;
+  if (need_node_alias && g->nnz) {
+    if ((rc = dev_alloc(g, &d.node_J, g->nnz)) || (rc = dev_alloc(g, &d.node_q, g->nnz)) ||
+        (rc = dev_alloc(g, &stack, g->nnz)))
+      return rc;
+    k_alias_nodes<<<grid_for(g->n), kBlock>>>(g->n, d.offsets, d.weights, d.node_J, d.node_q, stack);
+    GW_HIP_TRY(hipGetLastError());
+    GW_HIP_TRY(hipDeviceSynchronize());
+    dev_free(stack);
+  }
+  if (mode == GW_N2V_REPLAY && g->nnz) {
+    int64_t* sz = nullptr;
+    if ((rc = dev_alloc(g, &d.edge_off, g->nnz + 1)) || (rc = dev_alloc(g, &sz, g->nnz + 1))) return rc;
+    k_edge_sizes<<<grid_for(g->nnz), kBlock>>>(g->nnz, d.nbrs, d.deg, sz);
+    GW_HIP_TRY(hipMemset(sz + g->nnz, 0, sizeof(int64_t)));
+    size_t tmp_bytes = 0;
+    GW_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, sz, d.edge_off, g->nnz + 1));
+    void* tmp = nullptr;
+    if ((rc = dev_alloc(g, (char**)&tmp, (int64_t)tmp_bytes + 1))) return rc;
+    GW_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, sz, d.edge_off, g->nnz + 1));
+    GW_HIP_TRY(hipDeviceSynchronize());
+    dev_free(tmp);
+    dev_free(sz);
+    int64_t total = 0;
+    GW_HIP_TRY(hipMemcpy(&total, d.edge_off + g->nnz, sizeof(int64_t), hipMemcpyDeviceToHost));
+    // sum(deg^2) tables: refuse beyond ~16 GB of tables
+    if (total > (int64_t)1 << 30) {
+      dev_free(d.edge_off);
+      g->err = "per-edge alias tables need " + std::to_string(total) +
+               " entries (sum of deg^2); use GW_N2V_REJECTION at this scale";
+      return GW_ERR_CAPACITY;
+    }
+    if ((rc = dev_alloc(g, &d.edge_J, total)) || (rc = dev_alloc(g, &d.edge_q, total)) ||
+        (rc = dev_alloc(g, &stack, total)))
+      return rc;
+    k_alias_edges<<<grid_for(g->nnz), kBlock>>>(g->n, g->nnz, d.offsets, d.nbrs, d.weights, p, q,
+                                                d.edge_off, d.edge_J, d.edge_q, stack);
+    GW_HIP_TRY(hipGetLastError());
+    GW_HIP_TRY(hipDeviceSynchronize());
+    dev_free(stack);
+    g->edge_alias_entries = total;
+  }
+  g->p = p;
+  g->q = q;
+  g->n2v_mode = mode;
+  g->n2v_prepared = 1;
+  return GW_OK;
+}
+
+int gw_dev_alias_setup(int device, const double* probs, int64_t K, int64_t* J,
+                       double* q, std::string* err) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+    *err = "no HIP device visible (libgraphwalk has no CPU fallback)";
+    return GW_ERR_DEVICE;
+  }
+  if (K <= 0) return GW_OK;
+  if (hipSetDevice(device) != hipSuccess) {
+    *err = "hipSetDevice failed";
+    return GW_ERR_DEVICE;
+  }
+  double *dp = nullptr, *dq = nullptr;
+  int64_t* dJ = nullptr;
+  int32_t* st = nullptr;
+  hipError_t e = hipMalloc((void**)&dp, K * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&dq, K * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&dJ, K * sizeof(int64_t));
+  if (e == hipSuccess) e = hipMalloc((void**)&st, K * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMemcpy(dp, probs, K * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    k_alias_single<<<1, 64>>>(dp, K, dJ, dq, st);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(J, dJ, K * sizeof(int64_t), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(q, dq, K * sizeof(double), hipMemcpyDeviceToHost);
+  if (dp) (void)hipFree(dp);
+  if (dq) (void)hipFree(dq);
+  if (dJ) (void)hipFree(dJ);
+  if (st) (void)hipFree(st);
+  if (e != hipSuccess) {
+    *err = hipGetErrorString(e);
+    return GW_ERR_DEVICE;
+  }
+  return GW_OK;
+}
+
+int gw_dev_n2v_walks_replay(gw_graph* g, int L, int64_t nwalks, const int32_t* starts,
+                            const double* uniforms, int64_t nU, int32_t* out_walks,
+                            int32_t* out_len, int64_t* used) {
+  GW_HIP_TRY(hipSetDevice(g->device));
+  int rc;
+  int32_t *d_starts = nullptr, *d_out = nullptr, *d_len = nullptr;
+  double* d_U = nullptr;
+  int64_t* d_uoff = nullptr;
+  int* d_over = nullptr;
+  auto cleanup = [&]() {
+    dev_free(d_starts);
+    dev_free(d_out);
+    dev_free(d_len);
+    dev_free(d_U);
+    dev_free(d_uoff);
+    dev_free(d_over);
+  };
+  if ((rc = dev_alloc(g, &d_starts, nwalks)) || (rc = dev_alloc(g, &d_out, nwalks * (int64_t)L)) ||
+      (rc = dev_alloc(g, &d_len, nwalks)) || (rc = dev_alloc(g, &d_U, std::max<int64_t>(nU, 1))) ||
+      (rc = dev_alloc(g, &d_uoff, nwalks)) || (rc = dev_alloc(g, &d_over, 1))) {
+    cleanup();
+    return rc;
+  }
+  GW_HIP_TRY(hipMemcpy(d_starts, starts, nwalks * sizeof(int32_t), hipMemcpyHostToDevice));
+  if (nU) GW_HIP_TRY(hipMemcpy(d_U, uniforms, nU * sizeof(double), hipMemcpyHostToDevice));
+  GW_HIP_TRY(hipMemset(d_over, 0, sizeof(int)));
+  // Offsets into the uniform stream: walk w starts after all draws of walks
+  // < w (2 per step).  Assume full-length walks; a walk that stops early at a
+  // sink shifts every later walk, so re-run from the first walk whose length
+  // differs until the lengths are a fixed point (each pass finalises at
+  // least one more walk; undirected graphs converge in one pass).
+  std::vector<int64_t> uoff(nwalks);
+  std::vector<int32_t> lens(nwalks, L);
+  for (int64_t w = 0; w < nwalks; ++w) {
+    // a start with no neighbours draws nothing
+    int64_t s = starts[w];
+    if (g->offsets[s + 1] == g->offsets[s]) lens[w] = 1;
+  }
+  std::vector<int32_t> got(nwalks);
+  int64_t first_unsettled = 0;
+  for (int pass = 0;; ++pass) {
+    int64_t acc = 0;
+    for (int64_t w = 0; w < nwalks; ++w) {
+      uoff[w] = acc;
+      acc += 2 * (int64_t)(lens[w] - 1);
+    }
+    GW_HIP_TRY(hipMemcpy(d_uoff, uoff.data(), nwalks * sizeof(int64_t), hipMemcpyHostToDevice));
+    GW_HIP_TRY(hipMemset(d_over, 0, sizeof(int)));  // speculative passes may overrun
+    const int64_t todo = nwalks - first_unsettled;
+    k_walk_replay<<<grid_for(todo), kBlock>>>(g->d, L, todo, d_starts + first_unsettled, d_U, nU,
+                                              d_uoff + first_unsettled, d_out + first_unsettled * (int64_t)L,
+                                              d_len + first_unsettled, d_over);
+    GW_HIP_TRY(hipGetLastError());
+    GW_HIP_TRY(hipMemcpy(got.data(), d_len, nwalks * sizeof(int32_t), hipMemcpyDeviceToHost));
+    int64_t mism = -1;
+    for (int64_t w = first_unsettled; w < nwalks; ++w)
+      if (got[w] != lens[w]) {
+        mism = w;
+        break;
+      }
+    if (mism < 0) {
+      int over = 0;
+      GW_HIP_TRY(hipMemcpy(&over, d_over, sizeof(int), hipMemcpyDeviceToHost));
+      if (over) {
+        cleanup();
+        g->err = "uniform stream exhausted (supply 2*(walk_len-1) uniforms per walk)";
+        return GW_ERR_INVALID;
+      }
+      if (used) *used = acc;
+      break;
+    }
+    // walks before mism used correct offsets; mism's own offset was correct
+    // too, so its length is final.  Re-plan everything after it.
+    for (int64_t w = first_unsettled; w <= mism; ++w) lens[w] = got[w];
+    first_unsettled = mism + 1;
+    if (first_unsettled >= nwalks) {
+      int64_t a2 = 0;
+      for (int64_t w = 0; w < nwalks; ++w) a2 += 2 * (int64_t)(lens[w] - 1);
+      if (used) *used = a2;
+      break;
+    }
+  }
+  GW_HIP_TRY(hipMemcpy(out_walks, d_out, nwalks * (int64_t)L * sizeof(int32_t), hipMemcpyDeviceToHost));
+  GW_HIP_TRY(hipMemcpy(out_len, d_len, nwalks * sizeof(int32_t), hipMemcpyDeviceToHost));
+  cleanup();
+  return GW_OK;
+}
+
+int gw_dev_n2v_walks(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int64_t walk_count,
+                     int shuffle, int32_t* out_dev, int32_t* len_dev, uint64_t* counters_dev,
+                     void* stream) {
+  if (walk_count <= 0) return GW_OK;
+  const bool first_order = (g->p == 1.0 && g->q == 1.0);
+  if (!first_order && g->semantics != GW_SEM_NX_SIMPLE) {
+    g->err = "second-order walks need sorted rows (NX_SIMPLE semantics)";
+    return GW_ERR_UNSUPPORTED;
+  }
+  N2VParams P;
+  P.a_p = 1.0 / g->p;
+  P.a_q = 1.0 / g->q;
+  P.M = std::max(1.0, P.a_q);
+  P.lo = std::min(1.0, P.a_q);
+  P.extra = P.a_p > P.M ? P.a_p - P.M : 0.0;
+  P.h_prev = std::min(P.a_p, P.M);
+  P.k0 = (uint32_t)seed;
+  P.k1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_STEP;
+  P.pk0 = (uint32_t)seed;
+  P.pk1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_PERM;
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned grid = grid_for(walk_count);
+  unsigned long long* C = (unsigned long long*)counters_dev;
+#define GW_LAUNCH(FO, WT, DI) \
+  k_walk_scale<FO, WT, DI><<<grid, kBlock, 0, s>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev, len_dev, C)
+  const bool wt = g->weighted != 0, di = g->directed != 0;
+  if (first_order) {
+    if (wt) GW_LAUNCH(true, true, false);
+    else GW_LAUNCH(true, false, false);
+  } else if (wt) {
+    if (di) GW_LAUNCH(false, true, true);
+    else GW_LAUNCH(false, true, false);
+  } else {
+    if (di) GW_LAUNCH(false, false, true);
+    else GW_LAUNCH(false, false, false);
+  }
+#undef GW_LAUNCH
+  GW_HIP_TRY(hipGetLastError());
+  return GW_OK;
+}
+
+int gw_hip_device_count(int* count) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *count = c;
+  return c > 0 ? GW_OK : GW_ERR_DEVICE;
+}
+
+extern "C" int gw_n2v_export_alias(const gw_graph* gc, int32_t* node_J, double* node_q,
+                                   int64_t* edge_off, int32_t* edge_J, double* edge_q) {
+  gw_graph* g = const_cast<gw_graph*>(gc);
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  if (!g->n2v_prepared) return gw_fail(g, GW_ERR_STATE, "call gw_n2v_prepare first");
+  GW_HIP_TRY(hipSetDevice(g->device));
+  const gw_dev_graph& d = g->d;
+  if ((node_J || node_q) && !d.node_J)
+    return gw_fail(g, GW_ERR_STATE, "no per-node alias tables (unweighted REJECTION mode draws uniformly)");
+  if (node_J && g->nnz) GW_HIP_TRY(hipMemcpy(node_J, d.node_J, sizeof(int32_t) * g->nnz, hipMemcpyDeviceToHost));
+  if (node_q && g->nnz) GW_HIP_TRY(hipMemcpy(node_q, d.node_q, sizeof(double) * g->nnz, hipMemcpyDeviceToHost));
+  if (edge_off || edge_J || edge_q) {
+    if (g->n2v_mode != GW_N2V_REPLAY) return gw_fail(g, GW_ERR_STATE, "per-edge tables exist only in GW_N2V_REPLAY mode");
+    if (edge_off) GW_HIP_TRY(hipMemcpy(edge_off, d.edge_off, sizeof(int64_t) * (g->nnz + 1), hipMemcpyDeviceToHost));
+    if (edge_J && g->edge_alias_entries)
+      GW_HIP_TRY(hipMemcpy(edge_J, d.edge_J, sizeof(int32_t) * g->edge_alias_entries, hipMemcpyDeviceToHost));
+    if (edge_q && g->edge_alias_entries)
+      GW_HIP_TRY(hipMemcpy(edge_q, d.edge_q, sizeof(double) * g->edge_alias_entries, hipMemcpyDeviceToHost));
+  }
+  return GW_OK;
+}

@@ -1,0 +1,761 @@
+// TopSim random-walk SimRank on gfx950 (H2).
+//
+// Reference: DeepSim/TopSimAll/src/simrank/TopSim_singleSample.java
+//   ctor/compute   :35-54   cache[i] = C^i, one walk() per source, sim[i][i]=0
+//   walk           :62-158  level-synchronous expansion of weighted paths:
+//                           mass >= degree  -> enumerate all neighbours, mass/d
+//                           else            -> ceil(mass) random children,
+//                                              mass/ceil(mass) each
+//   computePathSim :167-203 at pathLen = 2i, every path with target != source
+//                           and isFirstMeet (:211-218) adds
+//                           ((mass * C^i) * deg(mid)) / deg(target)
+// plus TopSim_Enumerate.java:61-136 (always enumerate) and
+// SingleRandomWalk.java:53-92 (SAMPLE independent walks, score / SAMPLE),
+// and Print.printByOrder's per-row top-k (Print.java:25-53).
+//
+// Decomposition (one persistent workgroup per query source at a time):
+//   * the deterministic part of the path tree (nodes created by enumeration)
+//     is expanded level by level with workgroup scans; level arrays hold
+//     (vertex, parent) so any path is rebuilt by walking parents;
+//   * a node with mass < degree spawns ceil(mass) random children; each such
+//     child and all its descendants have mass <= 1 and exactly ONE child per
+//     level (mass stays m/ceil(m)), i.e. it is an independent random walk.
+//     Those walkers run one per lane with the path in registers, Philox keyed
+//     by (source, walker index, level), the walker index being the position
+//     in the reference's BFS queue order (level-major, queue order, child j);
+//   * pair updates accumulate in a dense fp64 row of the workgroup (LDS when
+//     n*8 fits, HBM otherwise with a touched list), then a radix select picks
+//     the top-k (score desc, id asc) and the row is re-zeroed.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "gw_device_common.h"
+
+namespace {
+
+constexpr int TS_BLOCK = 512;
+constexpr int TS_WAVES = TS_BLOCK / 64;
+constexpr int TOPK_MAX = 256;
+constexpr int64_t LDS_ROW_MAX_BYTES = 96 * 1024;
+
+struct TsArgs {
+  gw_dev_graph G;
+  int variant;
+  int sample;
+  double sampled;
+  double cache[16];
+  uint32_t k0, k1;
+  const int32_t* sources;
+  int64_t nsrc;
+  int topk;
+  int32_t* out_ids;
+  double* out_scores;
+  double* out_rows;
+  long long* stats;
+  int64_t level_cap, spawn_cap, touch_cap;
+  int32_t* lvl_vertex;
+  int32_t* lvl_parent;
+  double* lvl_mass;
+  int32_t* child_off;
+  int32_t* spawn_node;
+  int32_t* spawn_level;
+  int32_t* spawn_first;
+  double* spawn_mass;
+  double* acc_row;
+  int32_t* touched;
+  unsigned int* src_counter;
+  int* error_flag;
+};
+
+__device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_wave[wid] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int w = 0; w < TS_WAVES; ++w) {
+      int t = s_wave[w];
+      s_wave[w] = acc;
+      acc += t;
+    }
+    s_wave[TS_WAVES] = acc;
+  }
+  __syncthreads();
+  int r = s_wave[wid] + x - v;
+  *total = s_wave[TS_WAVES];
+  __syncthreads();
+  return r;
+}
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* s_red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  T r = 0;
+  for (int w = 0; w < TS_WAVES; ++w) r += s_red[w];
+  __syncthreads();
+  return r;
+}
+
+// first index i in [0, n) with a[i] > x  (a non-decreasing)
+__device__ __forceinline__ int upper_bound_i32(const int32_t* a, int n, int x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (a[mid] <= x)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ unsigned long long dkey(double v) {
+  return (unsigned long long)__double_as_longlong(v);  // v >= 0: bit order == value order
+}
+
+template <int STEP, bool LDS_ROW>
+__global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
+  constexpr int L = 2 * STEP;
+  extern __shared__ double s_row[];  // LDS accumulator row (LDS_ROW)
+  __shared__ int s_wave[TS_WAVES + 1];
+  __shared__ long long s_red[TS_WAVES];
+  __shared__ int s_size[L + 2];
+  __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort;
+  __shared__ unsigned s_hist[256];
+  __shared__ unsigned long long s_prefix, s_mask;
+  __shared__ int32_t s_sel_id[TOPK_MAX];
+  __shared__ double s_sel_val[TOPK_MAX];
+
+  const int tid = threadIdx.x;
+  const int64_t blk = blockIdx.x;
+  const gw_dev_graph& G = A.G;
+  const int n = (int)G.n;
+  const int64_t cap = A.level_cap;
+  int32_t* V = A.lvl_vertex + blk * (int64_t)(L + 1) * cap;
+  int32_t* P = A.lvl_parent + blk * (int64_t)(L + 1) * cap;
+  double* M = A.lvl_mass + blk * 2 * cap;
+  int32_t* CO = A.child_off + blk * (cap + 1);
+  int32_t* SN = A.spawn_node + blk * A.spawn_cap;
+  int32_t* SL = A.spawn_level + blk * A.spawn_cap;
+  int32_t* SF = A.spawn_first + blk * (A.spawn_cap + 1);
+  double* SM = A.spawn_mass + blk * A.spawn_cap;
+  double* acc = LDS_ROW ? s_row : (A.acc_row + blk * (int64_t)n);
+  int32_t* touched = LDS_ROW ? nullptr : (A.touched + blk * A.touch_cap);
+  const bool rw = (A.variant == GW_TOPSIM_SINGLE_RW);
+  const bool enumerate_all = (A.variant == GW_TOPSIM_ENUMERATE);
+
+  long long my_ext = 0, my_upd = 0, my_walk = 0, my_maxf = 0;
+
+  if (LDS_ROW)
+    for (int j = tid; j < n; j += TS_BLOCK) s_row[j] = 0.0;
+  if (tid == 0) s_ntouch = 0;
+  __syncthreads();
+
+  // accumulate one pair update into the row
+  auto add = [&](int32_t target, double val) {
+    if (LDS_ROW) {
+      atomicAdd(&acc[target], val);
+    } else {
+      double old = atomicAdd(&acc[target], val);
+      if (old == 0.0) {  // first touch (every update is > 0)
+        int k = atomicAdd(&s_ntouch, 1);
+        if (k < A.touch_cap)
+          touched[k] = target;
+        else
+          atomicOr(A.error_flag, 2);
+      }
+    }
+  };
+
+  // computePathSim for the path node at depth 2i with mass `mass`
+  auto contrib = [&](const int32_t* path, int i, int32_t source, double mass) {
+    const int32_t target = path[2 * i];
+    if (target == source) return;  // TopSim_singleSample.java:183
+#pragma unroll
+    for (int j = 0; j < STEP; ++j)  // isFirstMeet (:211-218)
+      if (j < i && path[j] == path[2 * i - j]) return;
+    const double dm = (double)G.deg[path[i]];
+    const double dt = (double)G.deg[target];
+    double val;
+    if (rw)  // SingleRandomWalk.java:89: cache[i]*deg/deg/SAMPLE
+      val = ((A.cache[i] * dm) / dt) / A.sampled;
+    else     // TopSim_singleSample.java:189
+      val = ((mass * A.cache[i]) * dm) / dt;
+    add(target, val);
+    ++my_upd;
+  };
+
+  for (;;) {
+    if (tid == 0) {
+      s_src = (int)atomicAdd(A.src_counter, 1u);
+      s_abort = 0;
+    }
+    __syncthreads();
+    const int64_t r = s_src;
+    if (r >= A.nsrc) break;
+    const int32_t s = A.sources[r];
+    const int ds = G.deg[s];
+
+    if (rw) {
+      if (tid == 0) {
+        s_nspawn = 0;
+        s_nwalk = 0;
+        if (ds > 0) {  // root spawns SAMPLE walks (SingleRandomWalk.java:55)
+          SL[0] = 0;
+          SN[0] = 0;
+          SM[0] = 1.0;
+          SF[0] = 0;
+          SF[1] = A.sample;
+          s_nspawn = 1;
+          s_nwalk = A.sample;
+        }
+      }
+      __syncthreads();
+    } else {
+      if (tid == 0) {
+        V[0] = s;
+        P[0] = -1;
+        M[0] = A.sampled;  // path[0].sample = SAMPLE (:73)
+        s_size[0] = 1;
+        s_nspawn = 0;
+      }
+      __syncthreads();
+      for (int l = 0; l <= L; ++l) {
+        const int sz = s_size[l];
+        const int32_t* Vl = V + (int64_t)l * cap;
+        const double* Ml = M + (int64_t)(l & 1) * cap;
+        if (tid == 0 && sz > my_maxf) my_maxf = sz;
+        // computePathSim at pathLen = 2i (:80-83, :157) for enumerated nodes
+        if ((l & 1) == 0 && l >= 2) {
+          for (int j = tid; j < sz; j += TS_BLOCK) {
+            int32_t path[L + 1];
+            int p = j;
+#pragma unroll
+            for (int t = L; t >= 1; --t) {
+              if (t <= l) {
+                path[t] = V[(int64_t)t * cap + p];
+                p = P[(int64_t)t * cap + p];
+              }
+            }
+            path[0] = s;
+#pragma unroll
+            for (int t = 2; t <= L; t += 2)
+              if (t == l) contrib(path, t / 2, s, Ml[j]);
+          }
+        }
+        if (l == L) break;
+        // expansion: child counts (enumerated) and spawners (random branch)
+        int total_children = 0;
+        int spawn_base = s_nspawn;
+        for (int base = 0; base < sz; base += TS_BLOCK) {
+          const int j = base + tid;
+          int cnt = 0, sp = 0;
+          double m = 0.0;
+          if (j < sz) {
+            const int32_t v = Vl[j];
+            const int d = G.deg[v];
+            m = Ml[j];
+            const bool det = enumerate_all ? (d != 0) : (d != 0 && m >= (double)d);  // :99
+            if (det)
+              cnt = d;
+            else if (d != 0)
+              sp = 1;  // d == 0: randNeighbor() == -1 -> no child (:143-144)
+          }
+          int tot_c, tot_s;
+          const int ex_c = block_excl_scan(cnt, s_wave, &tot_c);
+          const int ex_s = block_excl_scan(sp, s_wave, &tot_s);
+          if (j < sz) CO[j] = total_children + ex_c;
+          if (sp) {
+            const int k = spawn_base + ex_s;
+            if (k < A.spawn_cap) {
+              int c = (int)m;  // number = (int)s == s ? (int)s : (int)s + 1 (:131-135)
+              if ((double)c != m) c += 1;
+              SL[k] = l;
+              SN[k] = j;
+              SF[k] = c;
+              SM[k] = m / (double)c;  // (double)cur.sample/(double)number (:142)
+            } else {
+              atomicOr(A.error_flag, 1);
+              s_abort = 1;
+            }
+          }
+          total_children += tot_c;
+          spawn_base += tot_s;
+          if ((int64_t)total_children > cap) total_children = (int)cap + 1;  // saturate
+        }
+        if (tid == 0) {
+          CO[sz] = total_children;
+          s_nspawn = spawn_base;
+          if ((int64_t)total_children > cap) {
+            atomicOr(A.error_flag, 1);
+            s_abort = 1;
+          }
+        }
+        __syncthreads();
+        if (s_abort) break;
+        // load-balanced fill of level l+1 (BFS queue order)
+        int32_t* Vn = V + (int64_t)(l + 1) * cap;
+        int32_t* Pn = P + (int64_t)(l + 1) * cap;
+        double* Mn = M + (int64_t)((l + 1) & 1) * cap;
+        for (int c = tid; c < total_children; c += TS_BLOCK) {
+          const int j = upper_bound_i32(CO, sz + 1, c) - 1;
+          const int32_t v = Vl[j];
+          const int k = c - CO[j];
+          const int d = CO[j + 1] - CO[j];
+          Vn[c] = G.nbrs[G.offsets[v] + k];  // edges.get(j), insertion order (:103-110)
+          Pn[c] = j;
+          Mn[c] = Ml[j] / (double)d;         // newSample = cur.sample / degree (:104)
+        }
+        if (tid == 0) {
+          my_ext += total_children;
+          s_size[l + 1] = total_children;
+        }
+        __syncthreads();
+      }
+      // walker index prefix over spawners (queue order)
+      const int ns = s_abort ? 0 : s_nspawn;
+      int run = 0;
+      for (int base = 0; base < ns; base += TS_BLOCK) {
+        const int k = base + tid;
+        const int c = (k < ns) ? SF[k] : 0;
+        int tot;
+        const int ex = block_excl_scan(c, s_wave, &tot);
+        if (k < ns) SF[k] = run + ex;
+        run += tot;
+      }
+      if (tid == 0) {
+        SF[ns] = run;
+        s_nspawn = ns;
+        s_nwalk = run;
+      }
+      __syncthreads();
+    }
+
+    // random walkers: one lane each, path in registers
+    {
+      const int W = s_nwalk;
+      const int ns = s_nspawn;
+      for (int g = tid; g < W; g += TS_BLOCK) {
+        const int sp = upper_bound_i32(SF, ns + 1, g) - 1;
+        const int l0 = SL[sp];
+        const double mw = SM[sp];
+        int32_t path[L + 1];
+        int p = SN[sp];
+#pragma unroll
+        for (int t = L; t >= 1; --t) {
+          if (t <= l0) {
+            path[t] = V[(int64_t)t * cap + p];
+            p = P[(int64_t)t * cap + p];
+          }
+        }
+        path[0] = s;
+        int32_t cur = s;
+#pragma unroll
+        for (int t = 0; t <= L; ++t)
+          if (t == l0) cur = path[t];
+        bool alive = true;
+#pragma unroll
+        for (int t = 1; t <= L; ++t) {
+          if (t > l0 && alive) {
+            const int d = G.deg[cur];
+            if (d == 0) {
+              alive = false;
+            } else {
+              gw_u4 u = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)t, 0u, A.k0, A.k1);
+              cur = G.nbrs[G.offsets[cur] + gw_bounded(u.x, (uint32_t)d)];  // randNeighbor
+              path[t] = cur;
+              ++my_ext;
+              if ((t & 1) == 0) contrib(path, t / 2, s, mw);
+            }
+          }
+        }
+        ++my_walk;
+      }
+    }
+    __syncthreads();
+
+    // ---- output ------------------------------------------------------------
+    const int NC = LDS_ROW ? n : s_ntouch;
+    auto cand = [&](int idx, int32_t* id, double* val) -> bool {
+      int32_t t = LDS_ROW ? idx : touched[idx];
+      double v = acc[t];
+      *id = t;
+      *val = v;
+      return v > 0.0;
+    };
+    if (A.out_rows) {
+      double* orow = A.out_rows + r * (int64_t)n;
+      for (int t = tid; t < n; t += TS_BLOCK) orow[t] = acc[t];
+    }
+    if (A.out_ids) {
+      const int K = A.topk;
+      long long c_local = 0;
+      for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+        int32_t id;
+        double v;
+        if (cand(idx, &id, &v)) ++c_local;
+      }
+      const int C = (int)block_sum<long long>(c_local, s_red);
+      unsigned long long T = 0;  // threshold key (K-th largest)
+      int32_t idT = 0x7fffffff;  // largest id taken at key == T
+      bool take_all = (C <= K);
+      if (!take_all) {
+        if (tid == 0) {
+          s_prefix = 0;
+          s_mask = 0;
+          s_need = K;
+        }
+        __syncthreads();
+        for (int shift = 56; shift >= 0; shift -= 8) {
+          for (int b = tid; b < 256; b += TS_BLOCK) s_hist[b] = 0;
+          __syncthreads();
+          const unsigned long long pre = s_prefix, msk = s_mask;
+          for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+            int32_t id;
+            double v;
+            if (!cand(idx, &id, &v)) continue;
+            const unsigned long long k = dkey(v);
+            if ((k & msk) == pre) atomicAdd(&s_hist[(k >> shift) & 255], 1u);
+          }
+          __syncthreads();
+          if (tid == 0) {
+            int need = s_need, cum = 0, b = 255;
+            for (; b > 0; --b) {
+              if (cum + (int)s_hist[b] >= need) break;
+              cum += s_hist[b];
+            }
+            s_need = need - cum;
+            s_prefix = pre | ((unsigned long long)b << shift);
+            s_mask = msk | (255ull << shift);
+          }
+          __syncthreads();
+        }
+        T = s_prefix;
+        // ties at the threshold: smallest ids first
+        long long eq_local = 0;
+        for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+          int32_t id;
+          double v;
+          if (cand(idx, &id, &v) && dkey(v) == T) ++eq_local;
+        }
+        const int EQ = (int)block_sum<long long>(eq_local, s_red);
+        if (EQ > s_need) {
+          if (tid == 0) {
+            s_prefix = 0;
+            s_mask = 0;
+          }
+          __syncthreads();
+          for (int shift = 24; shift >= 0; shift -= 8) {
+            for (int b = tid; b < 256; b += TS_BLOCK) s_hist[b] = 0;
+            __syncthreads();
+            const unsigned long long pre = s_prefix, msk = s_mask;
+            for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+              int32_t id;
+              double v;
+              if (!cand(idx, &id, &v) || dkey(v) != T) continue;
+              const unsigned long long k = (unsigned)id;
+              if ((k & msk) == pre) atomicAdd(&s_hist[(k >> shift) & 255], 1u);
+            }
+            __syncthreads();
+            if (tid == 0) {
+              int need = s_need, cum = 0, b = 0;
+              for (; b < 255; ++b) {
+                if (cum + (int)s_hist[b] >= need) break;
+                cum += s_hist[b];
+              }
+              s_need = need - cum;
+              s_prefix = pre | ((unsigned long long)b << shift);
+              s_mask = msk | (255ull << shift);
+            }
+            __syncthreads();
+          }
+          idT = (int32_t)s_prefix;
+        }
+      }
+      if (tid == 0) s_cnt = 0;
+      __syncthreads();
+      for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+        int32_t id;
+        double v;
+        if (!cand(idx, &id, &v)) continue;
+        const unsigned long long k = dkey(v);
+        if (take_all || k > T || (k == T && id <= idT)) {
+          int slot = atomicAdd(&s_cnt, 1);
+          if (slot < TOPK_MAX) {
+            s_sel_id[slot] = id;
+            s_sel_val[slot] = v;
+          }
+        }
+      }
+      __syncthreads();
+      const int cnt = min(s_cnt, K);
+      // pad to a power of two and bitonic-sort by (value desc, id asc)
+      int P2 = 1;
+      while (P2 < cnt) P2 <<= 1;
+      for (int i = cnt + tid; i < P2; i += TS_BLOCK) {
+        s_sel_id[i] = 0x7fffffff;
+        s_sel_val[i] = -1.0;
+      }
+      __syncthreads();
+      for (int size = 2; size <= P2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+          for (int i = tid; i < P2; i += TS_BLOCK) {
+            const int jx = i ^ stride;
+            if (jx > i) {
+              const bool up = ((i & size) == 0);
+              const double vi = s_sel_val[i], vj = s_sel_val[jx];
+              const int32_t ii = s_sel_id[i], ij = s_sel_id[jx];
+              // "i before j" in final order: larger value, then smaller id
+              const bool i_first = (vi > vj) || (vi == vj && ii < ij);
+              if (i_first != up) {
+                s_sel_val[i] = vj;
+                s_sel_val[jx] = vi;
+                s_sel_id[i] = ij;
+                s_sel_id[jx] = ii;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+      int32_t* oid = A.out_ids + r * (int64_t)K;
+      double* osc = A.out_scores + r * (int64_t)K;
+      for (int k = tid; k < K; k += TS_BLOCK) {
+        oid[k] = k < cnt ? s_sel_id[k] : -1;
+        osc[k] = k < cnt ? s_sel_val[k] : 0.0;
+      }
+    }
+    __syncthreads();
+    // re-zero the accumulator for the next source
+    if (LDS_ROW) {
+      for (int t = tid; t < n; t += TS_BLOCK) s_row[t] = 0.0;
+    } else {
+      const int nt = min((int64_t)s_ntouch, A.touch_cap);
+      for (int k = tid; k < nt; k += TS_BLOCK) acc[touched[k]] = 0.0;
+    }
+    __syncthreads();
+    if (tid == 0) s_ntouch = 0;
+    __syncthreads();
+  }
+
+  // statistics
+  long long e = block_sum<long long>(my_ext, s_red);
+  long long u = block_sum<long long>(my_upd, s_red);
+  long long w = block_sum<long long>(my_walk, s_red);
+  if (tid == 0 && A.stats) {
+    atomicAdd((unsigned long long*)&A.stats[0], (unsigned long long)e);
+    atomicAdd((unsigned long long*)&A.stats[1], (unsigned long long)u);
+    atomicMax(&A.stats[2], my_maxf);
+    atomicAdd((unsigned long long*)&A.stats[3], (unsigned long long)w);
+  }
+}
+
+template <typename T>
+int ws_alloc(gw_graph* g, T** p, int64_t count) {
+  *p = nullptr;
+  if (count <= 0) count = 1;
+  hipError_t e = hipMalloc((void**)p, sizeof(T) * (size_t)count);
+  if (e != hipSuccess) {
+    g->err = std::string("hipMalloc(workspace ") + std::to_string(sizeof(T) * (size_t)count) + " B): " + hipGetErrorString(e);
+    *p = nullptr;
+    return GW_ERR_NOMEM;
+  }
+  return GW_OK;
+}
+
+template <typename T>
+void ws_free(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+template <int STEP, bool LDS>
+hipError_t launch_step(const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
+  if (LDS) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_topsim<STEP, LDS>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  k_topsim<STEP, LDS><<<blocks, TS_BLOCK, lds, s>>>(A);
+  return hipGetLastError();
+}
+
+template <bool LDS>
+hipError_t launch(int step, const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
+  switch (step) {
+    case 1: return launch_step<1, LDS>(A, blocks, lds, s);
+    case 2: return launch_step<2, LDS>(A, blocks, lds, s);
+    case 3: return launch_step<3, LDS>(A, blocks, lds, s);
+    case 4: return launch_step<4, LDS>(A, blocks, lds, s);
+    case 5: return launch_step<5, LDS>(A, blocks, lds, s);
+    case 6: return launch_step<6, LDS>(A, blocks, lds, s);
+    case 7: return launch_step<7, LDS>(A, blocks, lds, s);
+    case 8: return launch_step<8, LDS>(A, blocks, lds, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int topk) {
+  if (g->device < 0) {
+    g->err = "graph is not on a device (call gw_graph_to_device)";
+    return GW_ERR_STATE;
+  }
+  if (step < 1 || step > 8) {
+    g->err = "step must be in [1, 8]";
+    return GW_ERR_UNSUPPORTED;
+  }
+  if (sample < 1) {
+    g->err = "sample must be >= 1";
+    return GW_ERR_INVALID;
+  }
+  if (topk < 0 || topk > TOPK_MAX) {
+    g->err = "topk must be in [0, 256]";
+    return GW_ERR_UNSUPPORTED;
+  }
+  GW_HIP_TRY(hipSetDevice(g->device));
+  gw_topsim_ws& t = g->ts;
+  ws_free(t.lvl_vertex);
+  ws_free(t.lvl_parent);
+  ws_free(t.lvl_mass);
+  ws_free(t.child_off);
+  ws_free(t.spawn_node);
+  ws_free(t.spawn_level);
+  ws_free(t.spawn_first);
+  ws_free(t.spawn_mass);
+  ws_free(t.acc_row);
+  ws_free(t.touched);
+  ws_free(t.src_counter);
+  ws_free(t.error_flag);
+  const int64_t n = g->n;
+  const int L = 2 * step;
+  int64_t level_cap, spawn_cap;
+  if (variant == GW_TOPSIM_SINGLE_SAMPLE) {
+    level_cap = (int64_t)sample + 1;  // enumerated nodes carry mass >= 1
+    spawn_cap = (int64_t)sample + 1;
+  } else if (variant == GW_TOPSIM_ENUMERATE) {
+    level_cap = std::max<int64_t>((int64_t)sample + 1, 1 << 20);
+    spawn_cap = 1;
+  } else if (variant == GW_TOPSIM_SINGLE_RW) {
+    level_cap = 1;
+    spawn_cap = 1;
+  } else {
+    g->err = "unknown TopSim variant";
+    return GW_ERR_INVALID;
+  }
+  const bool lds_row = n * 8 <= LDS_ROW_MAX_BYTES;
+  const int64_t touch_cap = lds_row ? 1 : n;
+  const int64_t per_block = (int64_t)(L + 1) * level_cap * 8 + 2 * level_cap * 8 + (level_cap + 1) * 4 +
+                            spawn_cap * 20 + 4 + (lds_row ? 0 : n * 12);
+  int dev_cus = 256;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, g->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
+  const int64_t budget = (int64_t)16 << 30;  // 16 GB of the 288 GB HBM
+  int64_t blocks = std::min<int64_t>(4 * dev_cus, budget / std::max<int64_t>(per_block, 1));
+  if (variant == GW_TOPSIM_ENUMERATE) blocks = std::min<int64_t>(blocks, dev_cus);
+  if (blocks < 1) {
+    g->err = "TopSim workspace exceeds the 16 GB budget";
+    return GW_ERR_CAPACITY;
+  }
+  int rc;
+  if ((rc = ws_alloc(g, &t.lvl_vertex, blocks * (L + 1) * level_cap)) ||
+      (rc = ws_alloc(g, &t.lvl_parent, blocks * (L + 1) * level_cap)) ||
+      (rc = ws_alloc(g, &t.lvl_mass, blocks * 2 * level_cap)) ||
+      (rc = ws_alloc(g, &t.child_off, blocks * (level_cap + 1))) ||
+      (rc = ws_alloc(g, &t.spawn_node, blocks * spawn_cap)) ||
+      (rc = ws_alloc(g, &t.spawn_level, blocks * spawn_cap)) ||
+      (rc = ws_alloc(g, &t.spawn_first, blocks * (spawn_cap + 1))) ||
+      (rc = ws_alloc(g, &t.spawn_mass, blocks * spawn_cap)) ||
+      (rc = ws_alloc(g, &t.touched, blocks * touch_cap)) ||
+      (rc = ws_alloc(g, &t.src_counter, 1)) || (rc = ws_alloc(g, &t.error_flag, 1)))
+    return rc;
+  if (!lds_row) {
+    if ((rc = ws_alloc(g, &t.acc_row, blocks * n))) return rc;
+    GW_HIP_TRY(hipMemset(t.acc_row, 0, sizeof(double) * blocks * n));
+  }
+  t.variant = variant;
+  t.sample = sample;
+  t.step = step;
+  t.topk = topk;
+  t.blocks = (int)blocks;
+  t.level_cap = level_cap;
+  t.spawn_cap = spawn_cap;
+  t.touch_cap = touch_cap;
+  t.lds_row = lds_row ? 1 : 0;
+  t.lds_bytes = lds_row ? (size_t)n * 8 : 0;
+  GW_HIP_TRY(hipDeviceSynchronize());
+  return GW_OK;
+}
+
+int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint64_t seed,
+                  const int32_t* sources_dev, int64_t nsrc, int topk, int32_t* out_ids_dev,
+                  double* out_scores_dev, double* out_rows_dev, int64_t* stats_dev, void* stream) {
+  gw_topsim_ws& t = g->ts;
+  if (t.blocks == 0 || t.variant != variant || t.sample != sample || t.step != step ||
+      (out_ids_dev && topk > t.topk)) {
+    int rc = gw_dev_topsim_prepare(g, variant, sample, step, std::max(topk, t.topk > 0 ? t.topk : topk));
+    if (rc != GW_OK) return rc;
+  }
+  if (nsrc <= 0) return GW_OK;
+  GW_HIP_TRY(hipSetDevice(g->device));
+  hipStream_t s = (hipStream_t)stream;
+  TsArgs A;
+  A.G = g->d;
+  A.variant = variant;
+  A.sample = sample;
+  A.sampled = (double)sample;
+  for (int i = 0; i < 16; ++i) A.cache[i] = 0.0;
+  for (int i = 1; i <= step; ++i) A.cache[i] = std::pow(C, (double)i);  // Math.pow(C, i) (:43)
+  A.k0 = (uint32_t)seed;
+  A.k1 = (uint32_t)(seed >> 32) ^ GW_TAG_TOPSIM;
+  A.sources = sources_dev;
+  A.nsrc = nsrc;
+  A.topk = topk;
+  A.out_ids = out_ids_dev;
+  A.out_scores = out_scores_dev;
+  A.out_rows = out_rows_dev;
+  A.stats = (long long*)stats_dev;
+  A.level_cap = t.level_cap;
+  A.spawn_cap = t.spawn_cap;
+  A.touch_cap = t.touch_cap;
+  A.lvl_vertex = t.lvl_vertex;
+  A.lvl_parent = t.lvl_parent;
+  A.lvl_mass = t.lvl_mass;
+  A.child_off = t.child_off;
+  A.spawn_node = t.spawn_node;
+  A.spawn_level = t.spawn_level;
+  A.spawn_first = t.spawn_first;
+  A.spawn_mass = t.spawn_mass;
+  A.acc_row = t.acc_row;
+  A.touched = t.touched;
+  A.src_counter = t.src_counter;
+  A.error_flag = t.error_flag;
+  GW_HIP_TRY(hipMemsetAsync(t.src_counter, 0, sizeof(unsigned), s));
+  GW_HIP_TRY(hipMemsetAsync(t.error_flag, 0, sizeof(int), s));
+  const int blocks = (int)std::min<int64_t>(t.blocks, nsrc);
+  hipError_t e = t.lds_row ? launch<true>(step, A, blocks, t.lds_bytes, s)
+                           : launch<false>(step, A, blocks, 0, s);
+  if (e != hipSuccess) {
+    g->err = std::string("k_topsim launch: ") + hipGetErrorString(e);
+    return GW_ERR_DEVICE;
+  }
+  int flag = 0;
+  GW_HIP_TRY(hipMemcpyAsync(&flag, t.error_flag, sizeof(int), hipMemcpyDeviceToHost, s));
+  GW_HIP_TRY(hipStreamSynchronize(s));
+  if (flag) {
+    g->err = "TopSim frontier exceeded the workspace (level/spawn/touch capacity)";
+    return GW_ERR_CAPACITY;
+  }
+  return GW_OK;
+}

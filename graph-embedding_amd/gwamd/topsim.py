@@ -1,0 +1,213 @@
+"""Drop-in for the reference's TopSim side (DeepSim/TopSimAll/src), GPU-backed.
+
+    g = Graph(path, V, separator=",")              # structures.Graph (Graph.java:28-42)
+    ts = TopSim_singleSample(g, sample, step)     # TopSim_singleSample.java:35-44
+    ts.compute()                                  # :47-54 (all sources, on the GPU)
+    sim = ts.getResult()                          # :235-237 dense V x V (small V only)
+    ids, scores = ts.topK(k)                      # sparse top-k rows (any V)
+    printByOrder(ts, outPath, topk, testTopK)     # utils/Print.java:25-53
+    precision(gold, test, prePath, K)             # utils/Eval.java:81-131
+
+`TopSim_Enumerate` (TopSim_Enumerate.java, walks source 0 only by default)
+and `SingleRandomWalk` (SingleRandomWalk.java) use the same kernel.
+
+Randomness: the reference draws from an unseeded static java.util.Random
+(Graph.java:17); here every random child is a Philox draw keyed by
+(seed, source, walker index, level), so runs are reproducible.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib as C
+from .graph import GWGraph
+
+MIN = 0.000000001   # MyConfiguration.MIN (MyConfiguration.java:20)
+C_DEFAULT = 0.6     # MyConfiguration.C (:21)
+TOPK = 20           # MyConfiguration.TOPK (:19)
+SEPARATOR = ","     # MyConfiguration.SEPARATOR (:16)
+DENSE_LIMIT = 1 << 28  # bytes of dense result a getResult() may allocate
+
+
+class Graph:
+    """structures.Graph: undirected multigraph, insertion-order adjacency."""
+
+    def __init__(self, graphPath, V, separator=SEPARATOR, device=0):
+        self.vCount = int(V)
+        self._g = GWGraph.from_edgelist(graphPath, delimiter=separator, semantics="java",
+                                        vcount=int(V))
+        csr = self._g.export_csr()
+        self._offs = csr["offsets"]
+        self._nbrs = csr["nbrs"]
+        self.eCount = len(self._nbrs) // 2
+        self.device = device
+        self._on_device = False
+
+    def _ensure_device(self):
+        if not self._on_device:
+            self._g.to_device(self.device)
+            self._on_device = True
+
+    def degree(self, v):
+        return int(self._offs[v + 1] - self._offs[v])
+
+    def neighbors(self, v):
+        return self._nbrs[self._offs[v]:self._offs[v + 1]].tolist()
+
+    def getVCount(self):
+        return self.vCount
+
+    def getECount(self):
+        return self.eCount
+
+
+class _TopSimBase:
+    VARIANT = C.TOPSIM_SINGLE_SAMPLE
+
+    def __init__(self, g, sample, step, C_=C_DEFAULT, seed=0):
+        self.g = g
+        self.SAMPLE = int(sample)
+        self.STEP = int(step)
+        self.C = float(C_)
+        self.seed = int(seed)
+        self.COUNT = g.getVCount()
+        self.stats = None
+        self._sources = None
+        self._rows = None
+        self._topk = None
+
+    def _default_sources(self):
+        return np.arange(self.COUNT, dtype=np.int32)
+
+    def _run(self, sources, topk=None, dense=False):
+        import torch
+        g = self.g
+        g._ensure_device()
+        dev = torch.device("cuda", g.device)
+        src = torch.as_tensor(np.ascontiguousarray(sources, np.int32), device=dev)
+        stats = torch.zeros(4, dtype=torch.int64, device=dev)
+        h = g._g.handle
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        if dense:
+            rows = torch.empty((len(src), self.COUNT), dtype=torch.float64, device=dev)
+            C.check(C.lib().gw_topsim_dense(h, self.VARIANT, self.SAMPLE, self.STEP, self.C, self.seed,
+                                            C.ptr(src), len(src), C.ptr(rows), C.ptr(stats), stream), h)
+            out = rows.cpu().numpy()
+        else:
+            k = int(topk)
+            ids = torch.empty((len(src), k), dtype=torch.int32, device=dev)
+            sc = torch.empty((len(src), k), dtype=torch.float64, device=dev)
+            C.check(C.lib().gw_topsim(h, self.VARIANT, self.SAMPLE, self.STEP, self.C, self.seed,
+                                      C.ptr(src), len(src), k, C.ptr(ids), C.ptr(sc), C.ptr(stats), stream), h)
+            out = (ids.cpu().numpy(), sc.cpu().numpy())
+        s = stats.cpu().numpy()
+        self.stats = dict(extensions=int(s[0]), pair_updates=int(s[1]), max_frontier=int(s[2]),
+                          walkers=int(s[3]))
+        return out
+
+    def compute(self, sources=None):
+        """compute() over all sources (or the given ones).  Keeps dense rows
+        when they fit DENSE_LIMIT, else top-TOPK rows."""
+        src = self._default_sources() if sources is None else np.asarray(sources, np.int32)
+        self._sources = src
+        if len(src) * self.COUNT * 8 <= DENSE_LIMIT:
+            self._rows = self._run(src, dense=True)
+        else:
+            self._topk = self._run(src, topk=TOPK)
+
+    def getResult(self):
+        """double[V][V] (TopSim_singleSample.java:235); rows not computed are 0."""
+        if self._rows is None:
+            raise MemoryError("dense result too large for this graph; use topK()")
+        if len(self._sources) == self.COUNT and np.all(self._sources == np.arange(self.COUNT)):
+            return self._rows
+        full = np.zeros((self.COUNT, self.COUNT))
+        full[self._sources] = self._rows
+        return full
+
+    def topK(self, k=TOPK, sources=None):
+        src = self._default_sources() if sources is None else np.asarray(sources, np.int32)
+        return self._run(src, topk=k)
+
+
+class TopSim_singleSample(_TopSimBase):
+    VARIANT = C.TOPSIM_SINGLE_SAMPLE
+
+
+class TopSim_Basic(TopSim_singleSample):
+    """TopSim_Basic.java: the same algorithm as TopSim_singleSample."""
+
+
+class TopSim_Enumerate(_TopSimBase):
+    """TopSim_Enumerate.java:46-53: compute() walks source 0 only."""
+    VARIANT = C.TOPSIM_ENUMERATE
+
+    def _default_sources(self):
+        return np.array([0], np.int32)
+
+    def getResult(self):
+        full = np.zeros((self.COUNT, self.COUNT))
+        full[self._sources] = self._rows
+        return full
+
+
+class SingleRandomWalk(_TopSimBase):
+    """SingleRandomWalk.java:28-92 (scores divided by SAMPLE)."""
+    VARIANT = C.TOPSIM_SINGLE_RW
+
+
+def printByOrder(sim, outPath, topk=TOPK, testTopK=None, separator=SEPARATOR, decimals=6):
+    """Print.printByOrder (Print.java:25-53): `outPath` gets "v,id,...\\r\\n" and
+    `outPath.sim.txt` gets "v,id:%.6f,...\\r\\n".  `sim` is a dense V x V array
+    (exact Java FixedMaxPQ tie order and %.6f HALF_UP) or a TopSim object."""
+    if isinstance(sim, _TopSimBase):
+        if sim._rows is not None:
+            rows, ids = sim._rows, sim._sources
+            rows = np.ascontiguousarray(rows, np.float64)
+            C.check(C.lib().gw_write_sim_text_dense(str(outPath).encode(), C.ptr(rows),
+                                                    C.ptr(np.ascontiguousarray(ids, np.int32)),
+                                                    rows.shape[0], rows.shape[1], int(topk),
+                                                    separator.encode(), int(decimals)))
+            return
+        ids, sc = sim._topk if sim._topk is not None else sim.topK(topk)
+        ids = np.ascontiguousarray(ids, np.int32)
+        sc = np.ascontiguousarray(sc, np.float64)
+        rid = np.ascontiguousarray(sim._sources if sim._sources is not None else np.arange(ids.shape[0]),
+                                   np.int32)
+        C.check(C.lib().gw_write_sim_text_topk(str(outPath).encode(), C.ptr(ids), C.ptr(sc), C.ptr(rid),
+                                               ids.shape[0], ids.shape[1], separator.encode(),
+                                               int(decimals)))
+        return
+    rows = np.ascontiguousarray(sim, np.float64)
+    C.check(C.lib().gw_write_sim_text_dense(str(outPath).encode(), C.ptr(rows), None, rows.shape[0],
+                                            rows.shape[1], int(topk), separator.encode(), int(decimals)))
+
+
+def precision(path1, path2, prePath, K, separator=SEPARATOR, topk=TOPK):
+    """Eval.precision (Eval.java:81-131): mean over rows of
+    |gold ∩ test| / min(TOPK, |gold|) with ids whose score >= MIN; 1.0 when
+    the gold row is empty.  Writes "v,pre\\r\\n" lines to prePath."""
+    total, s, mn = 0, 0.0, float("inf")
+    with open(path1) as f1, open(path2) as f2, open(prePath, "w", newline="") as out:
+        for line1 in f1:
+            line2 = f2.readline()
+            line1 = line1.rstrip("\r\n")
+            line2 = line2.rstrip("\r\n")
+            t1 = [t for t in line1.split(separator)]
+            t2 = [t for t in line2.split(separator)]
+            while t1 and t1[-1] == "":
+                t1.pop()
+            while t2 and t2[-1] == "":
+                t2.pop()
+            if t1[0] != t2[0]:
+                print("error !" + t1[0] + "\t" + t2[0])
+                continue
+            s1 = {x.split(":")[0] for x in t1[1:] if float(x.split(":")[1]) >= MIN}
+            s2 = {x.split(":")[0] for x in t2[1:] if float(x.split(":")[1]) >= MIN}
+            realK = min(topk, len(s1))
+            pre = 1.0 if realK == 0 else len(s1 & s2) / realK
+            s += pre
+            out.write(f"{t1[0]}{separator}{pre}\r\n")
+            total += 1
+            mn = min(mn, pre)
+    return s / total if total else float("nan")

@@ -1,0 +1,224 @@
+/*
+ * graphwalk.h — C ABI of the MI355X-native node2vec walk generator (H1) and
+ * TopSim random-walk SimRank (H2).
+ *
+ * Drop-in boundary.  The reference has no FFI on this path; its interfaces are
+ * a Python class (H1) and Java classes (H2).  Every entry point below names
+ * the reference symbol it replaces (file:line relative to the reference
+ * checkout).  A maintainer binds these from Python with ctypes (see
+ * graph-embedding_amd/gwamd/_lib.py) or from Java with the JNI stub shown in
+ * INTEGRATION.md.
+ *
+ * Conventions
+ *   - plain C types only; opaque handles; every call returns an int status
+ *     (GW_OK == 0, negative = error); gw_last_error() gives the message.
+ *   - no global mutable state: seeds, modes and device ordinals are explicit;
+ *     one handle may be used from one thread at a time.
+ *   - "_dev" pointers are device (HBM) pointers, "stream" is a hipStream_t
+ *     (NULL = the default stream); such calls are asynchronous and launch-only
+ *     (no allocation, no synchronisation) so they can be captured in a graph.
+ *   - all other pointers are host pointers, caller-allocated; size them with
+ *     gw_graph_info() / the documented formulas.
+ *   - vertex ids crossing the boundary are dense ids in [0, n) unless a
+ *     function says "labels"; gw_graph_export_csr() gives the label map.
+ */
+#ifndef GRAPHWALK_H
+#define GRAPHWALK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------- */
+#define GW_OK 0
+#define GW_ERR_INVALID (-1)     /* bad argument (Python ValueError)            */
+#define GW_ERR_IO (-2)          /* file open/read/write (Java IOException)     */
+#define GW_ERR_PARSE (-3)       /* malformed edge line (NumberFormatException) */
+#define GW_ERR_NOMEM (-4)       /* host or device allocation failed            */
+#define GW_ERR_DEVICE (-5)      /* HIP runtime error / no GPU                  */
+#define GW_ERR_STATE (-6)       /* call order (e.g. walks before prepare)      */
+#define GW_ERR_UNSUPPORTED (-7) /* option not supported for this graph/mode    */
+#define GW_ERR_RANGE (-8)       /* id out of [0,V) (ArrayIndexOutOfBounds)     */
+#define GW_ERR_KEY (-9)         /* missing edge key (Python KeyError)          */
+#define GW_ERR_ZERODIV (-10)    /* weights sum to 0 (ZeroDivisionError)        */
+#define GW_ERR_CAPACITY (-11)   /* workspace too small for the frontier        */
+
+/* ---- graph semantics ------------------------------ */
+/* networkx simple graph as built by read_graph (node2vec/src/main.py:76-89):
+ * duplicates merge (last weight wins, to_undirected resolves reciprocal pairs
+ * by node order), node order = first appearance, neighbours sorted by label,
+ * original integer labels kept.                                             */
+#define GW_SEM_NX_SIMPLE 0
+/* structures.Graph (DeepSim/TopSimAll/src/structures/Graph.java:28-57): each
+ * line appends both directions, duplicates kept, insertion order, ids dense
+ * in [0,V), V given by the caller.                                          */
+#define GW_SEM_JAVA_MULTI 1
+
+/* ---- node2vec modes ------------------------------------------------------ */
+/* exact reference replay: per-node AND per-edge alias tables
+ * (node2vec.py:83-113), uniforms supplied by the caller (MT19937 stream of
+ * np.random, node2vec.py:156-157).  Needs sum(deg^2) table entries.        */
+#define GW_N2V_REPLAY 0
+/* scale mode: per-node alias only (or none when unweighted); second-order
+ * bias by exact rejection sampling with the return edge as an outlier;
+ * Philox4x32-10 keyed by (seed, walk, step, trial).                        */
+#define GW_N2V_REJECTION 1
+
+/* ---- TopSim variants (DeepSim/TopSimAll/src/simrank/) --------------------- */
+#define GW_TOPSIM_SINGLE_SAMPLE 0 /* TopSim_singleSample.java:62-203 (= _Basic) */
+#define GW_TOPSIM_ENUMERATE 1     /* TopSim_Enumerate.java:61-136 (always enumerate) */
+#define GW_TOPSIM_SINGLE_RW 2     /* SingleRandomWalk.java:53-92 (plain Monte-Carlo) */
+
+typedef struct gw_graph gw_graph;
+
+typedef struct gw_graph_info_t {
+  int64_t n;          /* vertices (dense ids 0..n-1)                        */
+  int64_t nnz;        /* adjacency entries (directed slots)                 */
+  int64_t max_degree;
+  int64_t edge_alias_entries; /* sum over slots of deg(dst); 0 until prepared */
+  int32_t semantics;  /* GW_SEM_*                                           */
+  int32_t directed;
+  int32_t weighted;
+  int32_t device;     /* -1 when not resident                               */
+} gw_graph_info_t;
+
+typedef struct gw_topsim_stats_t {
+  int64_t extensions;   /* path extensions (queue.add, TopSim_singleSample.java:115,147) */
+  int64_t pair_updates; /* executions of TopSim_singleSample.java:189                     */
+  int64_t max_frontier; /* largest per-source level size seen                             */
+  int64_t walkers;      /* random children spawned (mass < degree branch)                 */
+} gw_topsim_stats_t;
+
+/* ---- library -------------------------------------------------------------- */
+const char* gw_version(void);
+/* message of the last failing call made with this handle (NULL: the last
+ * failing handle-less call on this thread).                                 */
+const char* gw_last_error(const gw_graph* g);
+const char* gw_strerror(int code);
+/* number of visible GPUs (0 and GW_ERR_DEVICE when none)                    */
+int gw_device_count(int* count);
+
+/* ---- graph construction (host) ------------------------------------------ */
+/* Replaces read_graph (node2vec/src/main.py:76-89, sem NX_SIMPLE) and
+ * new structures.Graph(path, V) (Graph.java:28-42, sem JAVA_MULTI).
+ * delim: separator string (NULL or "" = any whitespace, as nx delimiter=None).
+ * vcount: JAVA_MULTI only (ids must lie in [0,vcount)); pass -1 otherwise.  */
+int gw_graph_load_edgelist(const char* path, const char* delim, int semantics,
+                           int directed, int weighted, int64_t vcount,
+                           gw_graph** out);
+/* Same semantics from in-memory edge arrays (labels for NX_SIMPLE, dense ids
+ * for JAVA_MULTI).  w may be NULL (unweighted, every weight 1).             */
+int gw_graph_from_edges(int64_t m, const int64_t* src, const int64_t* dst,
+                        const double* w, int semantics, int directed,
+                        int64_t vcount, gw_graph** out);
+/* A graph whose semantics are already resolved by the caller (e.g. a
+ * networkx graph handed to node2vec.Graph, node2vec.py:7-11): CSR over dense
+ * ids with rows in draw order (NX_SIMPLE: sorted by dense id, dense id order
+ * == label order), weights[nnz] (NULL = unweighted), labels[n] (NULL =
+ * identity), node_order[n] = dense ids in G.nodes() order (NULL = 0..n-1). */
+int gw_graph_from_csr(int64_t n, const int64_t* offsets, const int32_t* nbrs,
+                      const double* weights, const int64_t* labels,
+                      const int32_t* node_order, int semantics, int directed,
+                      gw_graph** out);
+/* Graph500 R-MAT (a,b,c; d = 1-a-b-c), 2^scale vertices, edge_factor*2^scale
+ * generated edges, symmetrised, deduplicated, self-loops dropped, isolated
+ * vertices removed; NX_SIMPLE semantics, labels = generator ids.  Philox
+ * keyed by seed: identical on every host.                                   */
+int gw_graph_rmat(int scale, int edge_factor, double a, double b, double c,
+                  uint64_t seed, gw_graph** out);
+int gw_graph_info(const gw_graph* g, gw_graph_info_t* info);
+/* offsets[n+1], nbrs[nnz] (dense ids, row order = draw order), weights[nnz]
+ * (NULL ok), labels[n] (NULL ok), node_order[n] (dense ids in the
+ * reference's G.nodes() order; NULL ok).                                    */
+int gw_graph_export_csr(const gw_graph* g, int64_t* offsets, int32_t* nbrs,
+                        double* weights, int64_t* labels, int32_t* node_order);
+int gw_graph_free(gw_graph* g);
+
+/* Upload CSR (+degree, weight sums) to HBM of `device`.                     */
+int gw_graph_to_device(gw_graph* g, int device);
+
+/* ---- node2vec (H1) ------------------------------------------------------- */
+/* Replaces Graph.preprocess_transition_probs (node2vec.py:83-113): builds the
+ * alias tables on the GPU (alias_setup node2vec.py:116-147, get_alias_edge
+ * :61-81).  mode GW_N2V_REPLAY builds per-edge tables (bit-exact with the
+ * reference); GW_N2V_REJECTION builds only what rejection sampling needs.   */
+int gw_n2v_prepare(gw_graph* g, double p, double q, int mode);
+/* Copy the alias tables back (node2vec.py:112-113 alias_nodes/alias_edges):
+ * node_J/node_q [nnz] in CSR slot order; edge_off [nnz+1], edge_J/edge_q
+ * [edge_alias_entries] (REPLAY only; pass NULL to skip).                    */
+int gw_n2v_export_alias(const gw_graph* g, int32_t* node_J, double* node_q,
+                        int64_t* edge_off, int32_t* edge_J, double* edge_q);
+/* Standalone alias_setup (node2vec.py:116-147) of one distribution on the
+ * GPU: J[K], q[K] (J as int64 like np.int).                                 */
+int gw_alias_setup(int device, const double* probs, int64_t K, int64_t* J,
+                   double* q);
+
+/* Exact reference replay of Graph.simulate_walks/node2vec_walk
+ * (node2vec.py:13-59) for nwalks walks whose start vertices (dense ids, the
+ * shuffled orders concatenated iteration-major) are given, consuming the
+ * caller's uniform stream (np.random.rand() values in draw order, 2 per
+ * step).  Host buffers: out_walks[nwalks*walk_len] (dense ids, -1 padded),
+ * out_len[nwalks]; *uniforms_used = values consumed.  Requires
+ * gw_n2v_prepare(..., GW_N2V_REPLAY).                                        */
+int gw_n2v_walks_replay(gw_graph* g, int walk_len, int64_t nwalks,
+                        const int32_t* starts, const double* uniforms,
+                        int64_t n_uniforms, int32_t* out_walks, int32_t* out_len,
+                        int64_t* uniforms_used);
+
+/* Scale-mode walks (GW_N2V_REJECTION or REPLAY tables), device-resident.
+ * Global walk index w in [walk_begin, walk_begin+walk_count): iteration
+ * it = w / n, start = node_order[perm_it(w % n)] (shuffle != 0; perm is the
+ * keyed Feistel bijection) or node_order[w % n] (shuffle == 0).  Output
+ * row-major [walk_count][walk_len] dense ids (-1 padded), lens optional.
+ * counters_dev (optional, 2 x uint64): += steps taken, += rejection trials. */
+int gw_n2v_walks(gw_graph* g, int walk_len, uint64_t seed, int64_t walk_begin,
+                 int64_t walk_count, int shuffle, int32_t* out_walks_dev,
+                 int32_t* out_len_dev, uint64_t* counters_dev, void* stream);
+
+/* ---- TopSim (H2) ------------------------------------------------------------ */
+/* Allocate the per-workgroup workspace for up to `sample`/`step` (kept in the
+ * handle; sizes the level arrays and the accumulator rows).                 */
+int gw_topsim_prepare(gw_graph* g, int variant, int sample, int step, int topk);
+/* Replaces new TopSim_singleSample(g, sample, step).compute() +
+ * Print.printByOrder's per-row FixedMaxPQ (TopSim_singleSample.java:35-54,
+ * Print.java:25-53) for the given sources: out_ids_dev[nsrc*topk],
+ * out_scores_dev[nsrc*topk], rows sorted by score desc then id asc, padded
+ * with (-1, 0.0).  Scores are NOT divided by sample for SINGLE_SAMPLE /
+ * ENUMERATE (as the reference); SINGLE_RW divides (SingleRandomWalk.java:89).
+ * C: decay (MyConfiguration.C = 0.6).  stats_dev (optional, 4 x int64):
+ * gw_topsim_stats_t accumulated on the device.                              */
+int gw_topsim(gw_graph* g, int variant, int sample, int step, double C,
+              uint64_t seed, const int32_t* sources_dev, int64_t nsrc, int topk,
+              int32_t* out_ids_dev, double* out_scores_dev, int64_t* stats_dev,
+              void* stream);
+/* Dense rows for small graphs (getResult(), TopSim_singleSample.java:235):
+ * out_rows_dev[nsrc*n] doubles, row r = sim[sources[r]][*], diagonal 0.     */
+int gw_topsim_dense(gw_graph* g, int variant, int sample, int step, double C,
+                    uint64_t seed, const int32_t* sources_dev, int64_t nsrc,
+                    double* out_rows_dev, int64_t* stats_dev, void* stream);
+
+/* ---- output writers (host) ------------------------------------------------ */
+/* DeepSim save_list format (DeepSim/src/main.py:237-243): one walk per line,
+ * every label followed by '\t', then '\n'.  walks: dense ids (-1 padded).   */
+int gw_write_walks_text(const gw_graph* g, const char* path,
+                        const int32_t* walks, const int32_t* lens,
+                        int64_t nwalks, int walk_len);
+/* Print.printByOrder format (Print.java:25-53): per row "v,id,id,...\r\n" to
+ * path and "v,id:%.6f,...\r\n" to path+".sim.txt".  Rows come from dense
+ * score rows (java_exact: emulate FixedMaxPQ/PriorityQueue tie order and
+ * Java's HALF_UP %.6f exactly) given as [nrows][n] host doubles.            */
+int gw_write_sim_text_dense(const char* path, const double* rows,
+                            const int32_t* row_ids, int64_t nrows, int64_t n,
+                            int topk, const char* sep, int decimals);
+/* Same format from top-k rows (ids/scores as produced by gw_topsim).       */
+int gw_write_sim_text_topk(const char* path, const int32_t* ids,
+                           const double* scores, const int32_t* row_ids,
+                           int64_t nrows, int topk, const char* sep,
+                           int decimals);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GRAPHWALK_H */

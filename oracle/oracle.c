@@ -1,0 +1,573 @@
+/*
+ * oracle.c — CPU restatement of the reference algorithms on the hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load liboracle.so; nothing on the product
+ * path (graph-embedding_amd/) links or calls it.
+ *
+ * Each function names the reference lines it restates (paths relative to the
+ * reference checkout).  Pinning (see DESIGN.md "Oracle"):
+ *   - or_alias_setup / or_alias_nodes / or_alias_edges / or_walks_replay are
+ *     checked bit-for-bit against golden vectors produced by importing the
+ *     reference node2vec.py (oracle/gen_goldens.py -> tests/golden/).
+ *   - or_simrank_naive is checked against the reference's committed naive
+ *     SimRank output IsoMap_LE/data/0_333_5038_simrank_navie_top10.txt.sim.txt.
+ *   - or_topsim (deterministic regime) is checked against or_simrank_naive
+ *     truncated at STEP iterations (exact KAT).  In the random
+ *     regime the reference's RNG is an unseeded java.util.Random, so the
+ *     Philox-keyed restatement here is the GPU's parity target and
+ *     or_topsim_java (java.util.Random stream) is used statistically.
+ *   - or_walks_scale restates the scale-mode sampling design (rejection
+ *     sampling of the node2vec.py:61-81 bias); its distribution is checked
+ *     against exact per-edge probabilities in tests.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../graph-embedding_amd/csrc/gw_philox.h"
+
+/* ------------------------------------------------------------------------ */
+/* node2vec.py:116-147 alias_setup                                           */
+/* ------------------------------------------------------------------------ */
+void or_alias_setup(const double* probs, int64_t K, int64_t* J, double* q) {
+  int64_t* smaller = (int64_t*)malloc(sizeof(int64_t) * (K + 1));
+  int64_t* larger = (int64_t*)malloc(sizeof(int64_t) * (K + 1));
+  int64_t ns = 0, nl = 0;
+  for (int64_t kk = 0; kk < K; ++kk) { /* :127-132 */
+    J[kk] = 0;
+    q[kk] = (double)K * probs[kk];
+    if (q[kk] < 1.0)
+      smaller[ns++] = kk;
+    else
+      larger[nl++] = kk;
+  }
+  while (ns > 0 && nl > 0) { /* :134-143 */
+    int64_t small = smaller[--ns];
+    int64_t large = larger[--nl];
+    J[small] = large;
+    q[large] = q[large] + q[small] - 1.0;
+    if (q[large] < 1.0)
+      smaller[ns++] = large;
+    else
+      larger[nl++] = large;
+  }
+  free(smaller);
+  free(larger);
+}
+
+/* node2vec.py:91-97: per node, probs = w / sum(w) over sorted neighbours */
+void or_alias_nodes(int64_t n, const int64_t* off, const double* w, int64_t* J, double* q) {
+  for (int64_t v = 0; v < n; ++v) {
+    int64_t b = off[v], K = off[v + 1] - off[v];
+    if (!K) continue;
+    double norm = 0.0;
+    for (int64_t k = 0; k < K; ++k) norm += w ? w[b + k] : 1.0;
+    double* pr = (double*)malloc(sizeof(double) * K);
+    for (int64_t k = 0; k < K; ++k) pr[k] = (w ? w[b + k] : 1.0) / norm;
+    or_alias_setup(pr, K, J + b, q + b);
+    free(pr);
+  }
+}
+
+static int has_edge(const int64_t* off, const int32_t* nbrs, int32_t a, int32_t b) {
+  int64_t lo = off[a], hi = off[a + 1];
+  while (lo < hi) {
+    int64_t mid = (lo + hi) / 2;
+    if (nbrs[mid] < b)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo < off[a + 1] && nbrs[lo] == b;
+}
+
+/* sizes of the per-edge tables: slot e = (u -> v) holds a table over N(v) */
+int64_t or_alias_edges_offsets(int64_t n, const int64_t* off, const int32_t* nbrs, int64_t* eoff) {
+  int64_t acc = 0, e = 0;
+  for (int64_t u = 0; u < n; ++u)
+    for (int64_t k = off[u]; k < off[u + 1]; ++k, ++e) {
+      eoff[e] = acc;
+      acc += off[nbrs[k] + 1] - off[nbrs[k]];
+    }
+  eoff[e] = acc;
+  return acc;
+}
+
+/* node2vec.py:61-81 get_alias_edge for every slot (src=u, dst=v) */
+void or_alias_edges(int64_t n, const int64_t* off, const int32_t* nbrs, const double* w, double p,
+                    double q, const int64_t* eoff, int64_t* J, double* qq) {
+  int64_t e = 0;
+  for (int64_t src = 0; src < n; ++src)
+    for (int64_t k = off[src]; k < off[src + 1]; ++k, ++e) {
+      int32_t dst = nbrs[k];
+      int64_t db = off[dst], K = off[dst + 1] - off[dst];
+      if (!K) continue;
+      double* un = (double*)malloc(sizeof(double) * K);
+      double norm = 0.0;
+      for (int64_t j = 0; j < K; ++j) {
+        int32_t x = nbrs[db + j];
+        double wx = w ? w[db + j] : 1.0;
+        if (x == src)
+          un[j] = wx / p;
+        else if (has_edge(off, nbrs, x, (int32_t)src))
+          un[j] = wx;
+        else
+          un[j] = wx / q;
+        norm += un[j];
+      }
+      for (int64_t j = 0; j < K; ++j) un[j] = un[j] / norm;
+      or_alias_setup(un, K, J + eoff[e], qq + eoff[e]);
+      free(un);
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* node2vec.py:13-59 walks with a caller-supplied uniform stream (exact)     */
+/* sequential: walk w consumes its draws right after walk w-1                */
+/* ------------------------------------------------------------------------ */
+int64_t or_walks_replay(int64_t n, const int64_t* off, const int32_t* nbrs, const int64_t* nJ,
+                        const double* nq, const int64_t* eoff, const int64_t* eJ, const double* eq,
+                        int L, int64_t nwalks, const int32_t* starts, const double* U, int64_t nU,
+                        int32_t* out, int32_t* lens) {
+  (void)n;
+  int64_t o = 0;
+  for (int64_t w = 0; w < nwalks; ++w) {
+    int32_t* row = out + w * (int64_t)L;
+    int32_t cur = starts[w];
+    int len = 1;
+    int64_t slot = -1;
+    row[0] = cur;
+    while (len < L) { /* :23-38 */
+      int64_t b = off[cur], d = off[cur + 1] - off[cur];
+      if (d == 0) break;
+      if (o + 2 > nU) return -1;
+      double u1 = U[o++], u2 = U[o++];
+      int64_t kk = (int64_t)floor(u1 * (double)d); /* alias_draw :156 */
+      const int64_t* J;
+      const double* q;
+      if (len == 1) {
+        J = nJ + b;
+        q = nq + b;
+      } else {
+        J = eJ + eoff[slot];
+        q = eq + eoff[slot];
+      }
+      int64_t idx = (u2 < q[kk]) ? kk : J[kk]; /* :157-160 */
+      slot = b + idx;
+      cur = nbrs[slot];
+      row[len++] = cur;
+    }
+    for (int t = len; t < L; ++t) row[t] = -1;
+    lens[w] = len;
+  }
+  return o;
+}
+
+/* ------------------------------------------------------------------------ */
+/* scale mode (Philox): restatement of the sampling design used on the GPU:  */
+/* first-order proposal from the node distribution, exact second-order bias  */
+/* of node2vec.py:61-81 by rejection with the return edge as an outlier.     */
+/* ------------------------------------------------------------------------ */
+static int64_t find_slot(const int64_t* off, const int32_t* nbrs, int32_t row, int32_t key) {
+  int64_t lo = off[row], hi = off[row + 1];
+  while (lo < hi) {
+    int64_t mid = (lo + hi) / 2;
+    if (nbrs[mid] < key)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return (lo < off[row + 1] && nbrs[lo] == key) ? lo : -1;
+}
+
+void or_walks_scale(int64_t n, const int64_t* off, const int32_t* nbrs, const double* w,
+                    const double* wsum, const int32_t* nJ, const double* nq, const int32_t* order,
+                    int directed, double p, double q, uint64_t seed, int L, int64_t walk_begin,
+                    int64_t walk_count, int shuffle, int32_t* out, int32_t* lens, uint64_t* counters,
+                    int nthreads) {
+  const int first_order = (p == 1.0 && q == 1.0);
+  const double a_p = 1.0 / p, a_q = 1.0 / q;
+  const double M = a_q > 1.0 ? a_q : 1.0;
+  const double lo = a_q < 1.0 ? a_q : 1.0;
+  const double extra = a_p > M ? a_p - M : 0.0;
+  const double h_prev = a_p < M ? a_p : M;
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_STEP;
+  const uint32_t pk0 = (uint32_t)seed, pk1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_PERM;
+  uint64_t tot_steps = 0, tot_trials = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : tot_steps, tot_trials)
+#endif
+  for (int64_t i = 0; i < walk_count; ++i) {
+    const int64_t wi = walk_begin + i;
+    const uint64_t it = (uint64_t)wi / (uint64_t)n, pos = (uint64_t)wi % (uint64_t)n;
+    const uint64_t sp = shuffle ? gw_feistel_perm(pos, (uint64_t)n, pk0, pk1, (uint32_t)it) : pos;
+    int32_t cur = order[sp], prev = -1;
+    double w_back = 1.0;
+    int back_ok = 0;
+    int32_t* row = out + i * (int64_t)L;
+    row[0] = cur;
+    int len = 1;
+    const uint32_t c0 = (uint32_t)wi, c1 = (uint32_t)((uint64_t)wi >> 32);
+    while (len < L) {
+      const int64_t b = off[cur], d = off[cur + 1] - b;
+      if (d == 0) break;
+      int64_t slot;
+      int32_t next;
+      if (first_order || len == 1) {
+        struct gw_u4 u = gw_philox(c0, c1, (uint32_t)len, 0u, k0, k1);
+        ++tot_trials;
+        int64_t kk = gw_bounded(u.x, (uint32_t)d);
+        if (w) kk = (gw_u01(u.y) < nq[b + kk]) ? kk : nJ[b + kk];
+        slot = b + kk;
+        next = nbrs[slot];
+      } else {
+        const double Wc = w ? wsum[cur] : (double)d;
+        const double oa = (back_ok && extra > 0.0) ? extra * w_back : 0.0;
+        const double A = M * Wc + oa;
+        uint32_t trial = 0;
+        for (;;) {
+          struct gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, k0, k1);
+          ++trial;
+          if (oa > 0.0 && gw_u01(u.z) * A < oa) {
+            slot = -1;
+            next = prev;
+            break;
+          }
+          int64_t kk = gw_bounded(u.x, (uint32_t)d);
+          if (w) kk = (gw_u01(u.y) < nq[b + kk]) ? kk : nJ[b + kk];
+          const int64_t s = b + kk;
+          const int32_t x = nbrs[s];
+          const double t = gw_u01(u.w) * M;
+          int acc;
+          if (x == prev)
+            acc = t < h_prev;
+          else if (t < lo)
+            acc = 1;
+          else {
+            int adj = directed ? (find_slot(off, nbrs, x, prev) >= 0)
+                               : (find_slot(off, nbrs, prev, x) >= 0);
+            acc = t < (adj ? 1.0 : a_q);
+          }
+          if (acc || trial >= (1u << 24)) {
+            slot = s;
+            next = x;
+            break;
+          }
+        }
+        tot_trials += trial;
+      }
+      if (directed) {
+        if (!first_order && extra > 0.0) {
+          int64_t bs = find_slot(off, nbrs, next, cur);
+          back_ok = bs >= 0;
+          w_back = (back_ok && w) ? w[bs] : 1.0;
+        }
+      } else if (slot >= 0) {
+        back_ok = 1;
+        w_back = w ? w[slot] : 1.0;
+      }
+      prev = cur;
+      cur = next;
+      row[len++] = cur;
+    }
+    for (int t = len; t < L; ++t) row[t] = -1;
+    if (lens) lens[i] = len;
+    tot_steps += (uint64_t)(len - 1);
+  }
+  if (counters) {
+    counters[0] += tot_steps;
+    counters[1] += tot_trials;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* java.util.Random (JDK 8): LCG48, next(bits), nextInt(bound)               */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  uint64_t seed;
+} jrand;
+void or_jrand_init(jrand* r, int64_t s) { r->seed = ((uint64_t)s ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1); }
+static int32_t jrand_next(jrand* r, int bits) {
+  r->seed = (r->seed * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+  return (int32_t)(int64_t)(r->seed >> (48 - bits));
+}
+int32_t or_jrand_next_int(jrand* r, int32_t bound) {
+  if ((bound & -bound) == bound) return (int32_t)(((int64_t)bound * (int64_t)jrand_next(r, 31)) >> 31);
+  int32_t bits, val;
+  do {
+    bits = jrand_next(r, 31);
+    val = bits % bound;
+  } while (bits - val + (bound - 1) < 0);
+  return val;
+}
+/* exposed for tests: first k nextInt(bound) values from new Random(seed) */
+void or_jrand_sequence(int64_t seed, int32_t bound, int64_t k, int32_t* out) {
+  jrand r;
+  or_jrand_init(&r, seed);
+  for (int64_t i = 0; i < k; ++i) out[i] = or_jrand_next_int(&r, bound);
+}
+
+/* ------------------------------------------------------------------------ */
+/* TopSim_singleSample.walk / computePathSim (TopSim_singleSample.java:62-203)
+ * restated literally as a FIFO queue of paths, one source at a time.
+ * variant 0: singleSample (:99 mass >= degree -> enumerate; else ceil(mass)
+ *            random children), 1: Enumerate (TopSim_Enumerate.java:99
+ *            always enumerate), 2: SingleRandomWalk (SingleRandomWalk.java).
+ * rng 0: Philox keyed by (source, walker index, level) with walker indices
+ *        assigned in queue order when a path first takes the random branch;
+ * rng 1: java.util.Random stream (seeded with java_seed, shared across
+ *        sources in source order, as Graph.rand is static).               */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int32_t* cur;    /* [cap][L+1] */
+  double* mass;    /* [cap][L+1] */
+  int64_t* walker; /* [cap]      */
+  int64_t size, cap;
+} pqueue;
+
+static void pq_reserve(pqueue* q, int64_t need, int L) {
+  if (need <= q->cap) return;
+  int64_t nc = q->cap ? q->cap : 1024;
+  while (nc < need) nc *= 2;
+  q->cur = (int32_t*)realloc(q->cur, sizeof(int32_t) * nc * (L + 1));
+  q->mass = (double*)realloc(q->mass, sizeof(double) * nc * (L + 1));
+  q->walker = (int64_t*)realloc(q->walker, sizeof(int64_t) * nc);
+  q->cap = nc;
+}
+
+static int first_meet(const int32_t* path, int dst) { /* isFirstMeet(path, 0, dst) :211-218 */
+  int internal = dst / 2;
+  for (int i = 0; i < internal; ++i)
+    if (path[i] == path[dst - i]) return 0;
+  return 1;
+}
+
+typedef struct {
+  int64_t ext, upd, maxf, walkers;
+} tstats;
+
+static void topsim_one(const int64_t* off, const int32_t* nbrs, int variant, int SAMPLE, int STEP,
+                       const double* cache, uint32_t k0, uint32_t k1, int rng, jrand* jr, int32_t src,
+                       double* row, pqueue* A, pqueue* B, tstats* st) {
+  const int L = 2 * STEP;
+  if (variant == 2) { /* SingleRandomWalk.walk :53-72 + computePathSim :81-92 */
+    int32_t* path = (int32_t*)malloc(sizeof(int32_t) * (L + 1));
+    for (int64_t i = 0; i < SAMPLE; ++i) {
+      int pathLen = 0;
+      for (int t = 0; t <= L; ++t) path[t] = -1;
+      path[0] = src;
+      int32_t cur = src;
+      while (pathLen < L) {
+        int64_t d = off[cur + 1] - off[cur];
+        if (d == 0) break;
+        int64_t k;
+        if (rng == 0) {
+          struct gw_u4 u = gw_philox((uint32_t)src, (uint32_t)i, (uint32_t)(pathLen + 1), 0u, k0, k1);
+          k = gw_bounded(u.x, (uint32_t)d);
+        } else {
+          k = or_jrand_next_int(jr, (int32_t)d);
+        }
+        cur = nbrs[off[cur] + k];
+        path[++pathLen] = cur;
+        st->ext++;
+      }
+      st->walkers++;
+      if (pathLen == 0) continue;
+      for (int ii = 1; ii <= STEP && 2 * ii <= pathLen; ++ii) {
+        int32_t inter = path[ii], target = path[2 * ii];
+        if (target == src) continue;
+        if (first_meet(path, 2 * ii)) {
+          double dm = (double)(off[inter + 1] - off[inter]), dt = (double)(off[target + 1] - off[target]);
+          row[target] += ((cache[ii] * dm) / dt) / (double)SAMPLE;
+          st->upd++;
+        }
+      }
+    }
+    free(path);
+    return;
+  }
+  /* :65-74 */
+  A->size = 0;
+  pq_reserve(A, 1, L);
+  for (int t = 0; t <= L; ++t) {
+    A->cur[t] = -1;
+    A->mass[t] = 0.0;
+  }
+  A->cur[0] = src;
+  A->mass[0] = (double)SAMPLE;
+  A->walker[0] = -1;
+  A->size = 1;
+  int64_t next_walker = 0;
+  int pathLen = 0, TopSim = 1;
+  for (;;) {
+    if (pathLen >= L || pathLen / 2 == TopSim) {
+      /* computePathSim(queue, pathLen, TopSim) :167-196 */
+      if (pathLen > 0) {
+        for (int64_t pi = 0; pi < A->size; ++pi) {
+          const int32_t* path = A->cur + pi * (L + 1);
+          const double* mass = A->mass + pi * (L + 1);
+          int32_t source = path[0];
+          for (int i = TopSim; i <= STEP && 2 * i <= pathLen; ++i) {
+            int32_t inter = path[i], target = path[2 * i];
+            if (target == source) continue;
+            if (target == -1) continue;
+            if (first_meet(path, 2 * i)) {
+              double dm = (double)(off[inter + 1] - off[inter]);
+              double dt = (double)(off[target + 1] - off[target]);
+              row[target] += ((mass[2 * i] * cache[i]) * dm) / dt; /* :189 */
+              st->upd++;
+            }
+          }
+        }
+      }
+      if (pathLen >= L) break;
+      TopSim++;
+    }
+    if (A->size > st->maxf) st->maxf = A->size;
+    /* expand every queued path by one level (:84-153) */
+    B->size = 0;
+    for (int64_t pi = 0; pi < A->size; ++pi) {
+      const int32_t* path = A->cur + pi * (L + 1);
+      const double* mass = A->mass + pi * (L + 1);
+      int32_t cur = path[pathLen];
+      double s = mass[pathLen];
+      int64_t d = off[cur + 1] - off[cur];
+      int det = (variant == 1) ? (d != 0) : (d != 0 && s >= (double)d);
+      if (det) {
+        double ns = s / (double)d; /* :104 */
+        pq_reserve(B, B->size + d, L);
+        for (int64_t j = 0; j < d; ++j) {
+          int64_t c = B->size++;
+          memcpy(B->cur + c * (L + 1), path, sizeof(int32_t) * (L + 1));
+          memcpy(B->mass + c * (L + 1), mass, sizeof(double) * (L + 1));
+          B->cur[c * (L + 1) + pathLen + 1] = nbrs[off[cur] + j];
+          B->mass[c * (L + 1) + pathLen + 1] = ns;
+          B->walker[c] = A->walker[pi];
+          st->ext++;
+        }
+      } else {
+        int number = (int)s; /* :131-135 */
+        if ((double)number != s) number += 1;
+        double ns = s / (double)number; /* :142 */
+        for (int j = 0; j < number; ++j) {
+          if (d == 0) break; /* randNeighbor == -1 -> break (:143-144) */
+          int64_t wid = A->walker[pi] >= 0 ? A->walker[pi] : next_walker++;
+          if (A->walker[pi] < 0) st->walkers++;
+          int64_t k;
+          if (rng == 0) {
+            struct gw_u4 u = gw_philox((uint32_t)src, (uint32_t)wid, (uint32_t)(pathLen + 1), 0u, k0, k1);
+            k = gw_bounded(u.x, (uint32_t)d);
+          } else {
+            k = or_jrand_next_int(jr, (int32_t)d);
+          }
+          pq_reserve(B, B->size + 1, L);
+          int64_t c = B->size++;
+          memcpy(B->cur + c * (L + 1), path, sizeof(int32_t) * (L + 1));
+          memcpy(B->mass + c * (L + 1), mass, sizeof(double) * (L + 1));
+          B->cur[c * (L + 1) + pathLen + 1] = nbrs[off[cur] + k];
+          B->mass[c * (L + 1) + pathLen + 1] = ns;
+          B->walker[c] = wid;
+          st->ext++;
+        }
+      }
+    }
+    pqueue tmp = *A;
+    *A = *B;
+    *B = tmp;
+    pathLen++;
+  }
+  row[src] = 0.0; /* sim[i][i] = 0 (:52) */
+}
+
+/* rows[r*n + t] = sim[sources[r]][t]; stats: ext, upd, maxf, walkers */
+void or_topsim(int64_t n, const int64_t* off, const int32_t* nbrs, int variant, int sample, int step,
+               double C, uint64_t seed, int rng, int64_t java_seed, const int32_t* sources, int64_t nsrc,
+               double* rows, int64_t* stats, int nthreads) {
+  double cache[32];
+  for (int i = 0; i < 32; ++i) cache[i] = 0.0;
+  for (int i = 1; i <= step && i < 32; ++i) cache[i] = pow(C, (double)i); /* :42-43 */
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32) ^ GW_TAG_TOPSIM;
+  int64_t e = 0, u = 0, mf = 0, w = 0;
+  memset(rows, 0, sizeof(double) * nsrc * n);
+  if (rng == 1) { /* java stream: sequential over sources */
+    jrand jr;
+    or_jrand_init(&jr, java_seed);
+    pqueue A = {0}, B = {0};
+    tstats st = {0, 0, 0, 0};
+    for (int64_t r = 0; r < nsrc; ++r)
+      topsim_one(off, nbrs, variant, sample, step, cache, k0, k1, 1, &jr, sources[r], rows + r * n, &A, &B, &st);
+    e = st.ext;
+    u = st.upd;
+    mf = st.maxf;
+    w = st.walkers;
+    free(A.cur); free(A.mass); free(A.walker);
+    free(B.cur); free(B.mass); free(B.walker);
+  } else {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel reduction(+ : e, u, w) reduction(max : mf)
+#endif
+    {
+      pqueue A = {0}, B = {0};
+      tstats st = {0, 0, 0, 0};
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+      for (int64_t r = 0; r < nsrc; ++r)
+        topsim_one(off, nbrs, variant, sample, step, cache, k0, k1, 0, NULL, sources[r], rows + r * n, &A, &B, &st);
+      e += st.ext;
+      u += st.upd;
+      w += st.walkers;
+      if (st.maxf > mf) mf = st.maxf;
+      free(A.cur); free(A.mass); free(A.walker);
+      free(B.cur); free(B.mass); free(B.walker);
+    }
+  }
+  if (stats) {
+    stats[0] = e;
+    stats[1] = u;
+    stats[2] = mf;
+    stats[3] = w;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* naive SimRank (SimRank.java:21-77): `iters` Jacobi sweeps over the upper  */
+/* triangle, sim(v,v)=1 during the sweeps, 0 afterwards (postProcess :62-65) */
+/* ------------------------------------------------------------------------ */
+void or_simrank_naive(int64_t n, const int64_t* off, const int32_t* nbrs, double C, int iters,
+                      double* sim, int nthreads) {
+  double* tmp = (double*)calloc((size_t)(n * n), sizeof(double));
+  memset(sim, 0, sizeof(double) * n * n);
+  for (int64_t i = 0; i < n; ++i) sim[i * n + i] = tmp[i * n + i] = 1.0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+  for (int r = 0; r < iters; ++r) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+    for (int64_t i = 0; i < n; ++i)
+      for (int64_t j = i + 1; j < n; ++j) {
+        double v = 0.0;
+        int64_t di = off[i + 1] - off[i], dj = off[j + 1] - off[j];
+        if (di != 0 && dj != 0) {
+          double res = 0.0;
+          for (int64_t a = off[i]; a < off[i + 1]; ++a)
+            for (int64_t b = off[j]; b < off[j + 1]; ++b) res += sim[(int64_t)nbrs[a] * n + nbrs[b]];
+          v = C * res / (double)(di * dj); /* :76 */
+        }
+        tmp[i * n + j] = v;
+        tmp[j * n + i] = v;
+      }
+    memcpy(sim, tmp, sizeof(double) * n * n);
+  }
+  for (int64_t i = 0; i < n; ++i) sim[i * n + i] = 0.0;
+  free(tmp);
+}

@@ -1,0 +1,210 @@
+"""CPU: pin the oracle against the reference's golden vectors and fixtures.
+
+Golden vectors: tests/golden/n2v_*.npz, produced by oracle/gen_goldens.py which
+imports the reference node2vec.py.  SimRank fixture: the reference's committed
+IsoMap_LE/data/0_333_5038_simrank_navie_top10.txt.sim.txt.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import DATA, golden_index, load_golden
+
+CASES = golden_index()["cases"]
+
+
+def _case_id(c):
+    return c["file"]
+
+
+@pytest.mark.parametrize("case", CASES, ids=_case_id)
+def test_nx_semantics_restatement(case, oracle):
+    """read_graph (main.py:76-89) restated without networkx == golden CSR."""
+    g = load_golden(case["file"])
+    order, labels, offs, nbrs, w = oracle.read_graph_nx_semantics(
+        os.path.join(DATA, case["graph"]), case["delimiter"], case["weighted"], case["directed"])
+    np.testing.assert_array_equal(order, g["node_order"])
+    np.testing.assert_array_equal(labels, g["labels"])
+    np.testing.assert_array_equal(offs, g["offsets"])
+    np.testing.assert_array_equal(labels[nbrs], g["nbrs"])
+    np.testing.assert_array_equal(w, g["weights"])
+
+
+@pytest.mark.parametrize("case", CASES, ids=_case_id)
+def test_alias_tables_bitwise(case, oracle):
+    """alias_setup / preprocess_transition_probs (node2vec.py:83-147)."""
+    g = load_golden(case["file"])
+    rank = {int(x): i for i, x in enumerate(g["labels"])}
+    nbrs = np.array([rank[int(x)] for x in g["nbrs"]], np.int32)
+    w = g["weights"] if case["weighted"] else None
+    J, q = oracle.alias_nodes(g["offsets"], w)
+    np.testing.assert_array_equal(J, g["alias_node_J"])
+    assert q.tobytes() == g["alias_node_q"].tobytes()
+    eoff, eJ, eq = oracle.alias_edges(g["offsets"], nbrs, w, case["p"], case["q"])
+    if "alias_edge_J" in g:
+        np.testing.assert_array_equal(eoff, g["alias_edge_off"])
+        np.testing.assert_array_equal(eJ, g["alias_edge_J"])
+        assert eq.tobytes() == g["alias_edge_q"].tobytes()
+    else:
+        assert hashlib.sha256(eoff.tobytes()).digest() == bytes(g["alias_edge_off_sha256"])
+        assert hashlib.sha256(eJ.tobytes()).digest() == bytes(g["alias_edge_J_sha256"])
+        assert hashlib.sha256(eq.tobytes()).digest() == bytes(g["alias_edge_q_sha256"])
+
+
+@pytest.mark.parametrize("case", CASES, ids=_case_id)
+def test_walks_replay_bitwise(case, oracle):
+    """node2vec_walk/simulate_walks (node2vec.py:13-59) replayed from the
+    np.random stream == the reference's own walks."""
+    g = load_golden(case["file"])
+    rank = {int(x): i for i, x in enumerate(g["labels"])}
+    nbrs = np.array([rank[int(x)] for x in g["nbrs"]], np.int32)
+    w = g["weights"] if case["weighted"] else None
+    nJ, nq = oracle.alias_nodes(g["offsets"], w)
+    eoff, eJ, eq = oracle.alias_edges(g["offsets"], nbrs, w, case["p"], case["q"])
+    starts = np.array([rank[int(x)] for x in g["starts"]], np.int32)
+    L = case["walk_length"]
+    U = np.random.RandomState(case["seed"]).random_sample(2 * (L - 1) * len(starts))
+    np.testing.assert_array_equal(U[:len(g["uniforms"])], g["uniforms"])
+    out, lens, used = oracle.walks_replay(g["offsets"], nbrs, nJ, nq, eoff, eJ, eq, L, starts, U)
+    assert used >= 0
+    np.testing.assert_array_equal(lens, g["lens"])
+    assert used == 2 * int((g["lens"] - 1).sum())
+    lab = np.where(out >= 0, g["labels"][np.maximum(out, 0)], -1).astype(np.int64)
+    if case["full_walks"]:
+        np.testing.assert_array_equal(lab, g["walks"])
+    else:
+        np.testing.assert_array_equal(lab[:64], g["walks_head"])
+        np.testing.assert_array_equal(lab[-64:], g["walks_tail"])
+    assert hashlib.sha256(lab.tobytes()).hexdigest() == case["walks_sha256"]
+
+
+def test_alias_setup_known_answer(oracle):
+    """alias_setup on a hand-checkable distribution (node2vec.py:116-147)."""
+    J, q = oracle.alias_setup([0.1, 0.2, 0.3, 0.4])
+    # q = K*p = [.4,.8,1.2,1.6]; smaller=[0,1], larger=[2,3]
+    # pop 1 & 3: J[1]=3, q[3]=1.6+0.8-1=1.4 -> larger=[2,3]
+    # pop 0 & 3: J[0]=3, q[3]=1.4+0.4-1=0.8 -> smaller=[3]
+    # pop 3 & 2: J[3]=2, q[2]=1.2+0.8-1=1.0 -> larger=[2]
+    np.testing.assert_array_equal(J, [3, 3, 0, 2])
+    np.testing.assert_allclose(q, [0.4, 0.8, 1.0, 0.8], rtol=0, atol=1e-15)
+
+
+def _java_graph_csr(path, V, sep):
+    adj = [[] for _ in range(V)]
+    with open(path) as f:
+        for line in f:
+            a, b = line.rstrip("\r\n").split(sep)[:2]
+            adj[int(a)].append(int(b))
+            adj[int(b)].append(int(a))
+    offs = np.zeros(V + 1, np.int64)
+    offs[1:] = np.cumsum([len(x) for x in adj])
+    return offs, np.array([y for x in adj for y in x], np.int32)
+
+
+def test_naive_simrank_fixture(oracle):
+    """SimRank.java:36-77 restated == the reference's committed naive SimRank
+    output (C=0.8, 30 iterations, Java graph semantics, top-10, %.8f)."""
+    offs, nbrs = _java_graph_csr(os.path.join(DATA, "0_333_5038.txt"), 333, " ")
+    sim = oracle.simrank_naive(offs, nbrs, 0.8, 30, nthreads=8)
+    rows = 0
+    with open(os.path.join(DATA, "0_333_5038_simrank_navie_top10.txt.sim.txt")) as f:
+        for line in f:
+            toks = line.strip().split(" ")
+            v = int(toks[0])
+            pairs = [(int(t.split(":")[0]), float(t.split(":")[1])) for t in toks[1:]]
+            for (i, val) in pairs:
+                assert abs(sim[v, i] - val) <= 5.1e-9, (v, i, sim[v, i], val)
+            rows += 1
+            if not pairs:  # vertex with no similar vertex: empty row
+                assert sim[v].max() < 5e-9
+                continue
+            # the listed ids are a valid top-10 of the row (ties allowed)
+            kth = pairs[-1][1]
+            assert np.sum(sim[v] > kth + 1e-8) <= len(pairs)
+    assert rows == 333
+
+
+@pytest.mark.parametrize("step", [1, 2])
+def test_topsim_deterministic_kat(oracle, step):
+    """KAT: with SAMPLE large enough that every expansion
+    enumerates, TopSim_singleSample / SAMPLE == naive SimRank after STEP
+    Jacobi sweeps (C=0.6) on moreno (Java multigraph semantics)."""
+    offs, nbrs = _java_graph_csr(os.path.join(DATA, "moreno_crime_crime.txt"), 1380, "\t")
+    sample = 1000 if step == 1 else 200000
+    rows, st = oracle.topsim(offs, nbrs, 0, sample, step, C=0.6, seed=1, nthreads=8)
+    assert st["walkers"] == 0, "regime is not deterministic"
+    naive = oracle.simrank_naive(offs, nbrs, 0.6, step, nthreads=8)
+    np.testing.assert_allclose(rows / sample, naive, rtol=0, atol=1e-13)
+
+
+def test_topsim_enumerate_equals_singlesample_in_det_regime(oracle):
+    offs, nbrs = _java_graph_csr(os.path.join(DATA, "moreno_crime_crime.txt"), 1380, "\t")
+    a, _ = oracle.topsim(offs, nbrs, 0, 1000, 1, sources=np.arange(0, 1380, 7))
+    b, _ = oracle.topsim(offs, nbrs, 1, 1000, 1, sources=np.arange(0, 1380, 7))
+    np.testing.assert_array_equal(a, b)
+
+
+def test_java_random_lcg(oracle):
+    # new Random(42).nextInt() == -1170105035 (well-known JDK value)
+    mask = (1 << 48) - 1
+    s = (42 ^ 0x5DEECE66D) & mask
+    s = (s * 0x5DEECE66D + 0xB) & mask
+    v = s >> 16
+    v = v - (1 << 32) if v >= 1 << 31 else v
+    assert v == -1170105035
+    # power-of-two bound path: (bound * next(31)) >> 31
+    seq = oracle.jrand_sequence(42, 1 << 30, 3)
+    s = (42 ^ 0x5DEECE66D) & mask
+    exp = []
+    for _ in range(3):
+        s = (s * 0x5DEECE66D + 0xB) & mask
+        exp.append(((1 << 30) * (s >> 17)) >> 31)
+    np.testing.assert_array_equal(seq, exp)
+    # rejection path stays in range
+    r = oracle.jrand_sequence(7, 1000, 10000)
+    assert r.min() >= 0 and r.max() < 1000
+
+
+def test_java_format_and_pq(oracle):
+    f = oracle.java_format_fixed
+    assert f(0.0) == "0.000000"
+    assert f(0.1234565) == "0.123457"   # HALF_UP on the shortest repr digits
+    assert f(1.0000005) == "1.000001"   # C printf would give 1.000000
+    assert f(153.5) == "153.500000"
+    # FixedMaxPQ tie order: k=2, offers 1.0,1.0,2.0 -> root (id 0) evicted
+    got = oracle.java_fixed_max_pq_row([1.0, 1.0, 2.0], 2)
+    assert [i for i, _ in got] == [2, 1]
+
+
+@pytest.mark.slow
+def test_scale_walks_match_second_order_distribution(oracle):
+    """The rejection design reproduces the reference transition
+    probabilities (alias_edges, node2vec.py:61-81) in distribution."""
+    g = load_golden("n2v_karate_p0.25_q4_s0.npz")
+    rank = {int(x): i for i, x in enumerate(g["labels"])}
+    nbrs = np.array([rank[int(x)] for x in g["nbrs"]], np.int32)
+    offs = g["offsets"]
+    csr = dict(offsets=offs, nbrs=nbrs, weights=None, node_order=np.arange(len(offs) - 1, dtype=np.int32))
+    n = len(offs) - 1
+    out, lens, cnt = oracle.walks_scale(csr, 0.25, 4, seed=3, L=3, walk_begin=0, walk_count=n * 20000,
+                                        nthreads=8)
+    # exact P(next | prev, cur) from the reference formula
+    counts = {}
+    for a, b, c in out:
+        counts.setdefault((a, b), {}).setdefault(c, 0)
+        counts[(a, b)][c] += 1
+    worst = 0.0
+    for (a, b), dist in counts.items():
+        tot = sum(dist.values())
+        if tot < 4000:
+            continue
+        row = nbrs[offs[b]:offs[b + 1]]
+        un = np.array([1 / 0.25 if x == a else (1.0 if x in set(nbrs[offs[a]:offs[a + 1]]) else 1 / 4)
+                       for x in row])
+        pr = un / un.sum()
+        emp = np.array([dist.get(int(x), 0) for x in row]) / tot
+        sd = np.sqrt(pr * (1 - pr) / tot)
+        worst = max(worst, float(np.max(np.abs(emp - pr) / np.maximum(sd, 1e-12))))
+    assert worst < 5.5, worst
