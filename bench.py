@@ -1,0 +1,298 @@
+#!/usr/bin/env python3
+"""bench.py — node2vec walk-steps/s on MI355X (+ TopSim pair-updates/s).
+
+Headline (BASELINE.json configs[1]): node2vec p=0.25 q=4 on a synthetic
+Graph500 R-MAT scale-20 graph (a,b,c = 0.57,0.19,0.19, edge factor 16, seed
+42, symmetrised, deduplicated, no self loops), walk_length 80, 10 walks per
+node.  One "step" = one pass of the hot path over one batch: 10 walks from
+every vertex (6.47M walks, ~5.1e8 walk-steps) written to HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N>1: launched by torch.distributed.run, one rank per GPU.  The graph is
+replicated; each rank walks its own block of global walk indices (walks are
+a pure function of (seed, global walk index), so shards never overlap and
+need no collective).  `value` = walk-steps of all ranks / max-over-ranks
+time ("scaling": "weak").  `--allgather` adds the RCCL all-gather of the
+emitted walks (north_star option) inside the timed step.
+
+Also reported (same JSON line):
+  roofline      36 algorithmic bytes per walk-step / kernel time,
+                kernel time from HIP events on the launch stream; traffic from
+                the committed rocprofv3 PMC pass (profiles/), or null.
+  cpu_baseline  the oracle's C restatement of the same sampling (OpenMP),
+                timed on a bounded sample of the same workload (rank 0, N=1).
+  secondary     TopSim_singleSample on lshrank blog (STEP=5, SAMPLE=10000,
+                C=0.6, top-20, all 10,313 sources): pair-updates/s.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "graph-embedding_amd"))
+sys.path.insert(0, ROOT)
+
+BYTES_PER_STEP = 36       # row bounds 16 + alias q/J 12 + nbr 4 + walk write 4
+TOPSIM_B_EXT = 52         # per path-extension
+TOPSIM_B_UPD = 24         # per pair-update
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scale", type=int, default=20)
+    ap.add_argument("--edge-factor", type=int, default=16)
+    ap.add_argument("--p", type=float, default=0.25)
+    ap.add_argument("--q", type=float, default=4.0)
+    ap.add_argument("--walk-length", type=int, default=80)
+    ap.add_argument("--num-walks", type=int, default=10)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--allgather", action="store_true")
+    ap.add_argument("--no-topsim", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--topsim-sample", type=int, default=10000)
+    ap.add_argument("--topsim-step", type=int, default=5)
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(csr, args, sample_walk0):
+    """Oracle (C restatement, OpenMP) on a bounded sample of the same walks."""
+    import oracle
+    import numpy as np
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except Exception:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    c = dict(offsets=csr["offsets"], nbrs=csr["nbrs"], weights=None, node_order=csr["node_order"])
+    L = args.walk_length
+    nw = 20000
+    t0 = time.perf_counter()
+    _, lens, _ = oracle.walks_scale(c, args.p, args.q, args.seed, L, sample_walk0, nw, nthreads=cores)
+    dt = time.perf_counter() - t0
+    nw2 = int(min(3_000_000, max(nw, nw * args.cpu_seconds / max(dt, 1e-3))))
+    t0 = time.perf_counter()
+    _, lens, _ = oracle.walks_scale(c, args.p, args.q, args.seed, L, sample_walk0, nw2, nthreads=cores)
+    dt = time.perf_counter() - t0
+    steps = int((lens.astype(np.int64) - 1).sum())
+    return {"value": steps / dt, "unit": "walk-steps/s", "cores": cores, "kind": "port",
+            "sample": f"{nw2} walks ({steps} walk-steps) of the same R-MAT-{args.scale} p={args.p} q={args.q} "
+                      f"L={L} workload, oracle/oracle.c or_walks_scale, {dt:.1f} s",
+            "reference_python_context": "reference node2vec.py measured 41,266 walk-steps/s/core on "
+                                        "RMAT-12 in the build container (SURVEY §6); it cannot run at scale 20 "
+                                        "(per-edge alias tables need 7.0e10 entries)"}
+
+
+def load_traffic(tag, launch_steps):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary."""
+    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        e = d.get(tag)
+        if e and e.get("walk_steps_per_launch") == launch_steps:
+            return e["hbm_bytes_per_launch"]
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import gwamd
+    from gwamd import _lib as C
+    L = args.walk_length
+
+    # ---- graph (host build, replicated on every rank) ----
+    t0 = time.perf_counter()
+    G = gwamd.GWGraph.rmat(args.scale, args.edge_factor, 0.57, 0.19, 0.19, args.seed)
+    inf = G.info()
+    n, nnz = inf.n, inf.nnz
+    log(f"[rank {rank}] rmat-{args.scale}: n={n} nnz={nnz} maxdeg={inf.max_degree} "
+        f"built in {time.perf_counter() - t0:.1f}s")
+    G.to_device(dev.index)
+    C.check(C.lib().gw_n2v_prepare(G.handle, args.p, args.q, C.N2V_REJECTION), G.handle)
+
+    B = args.num_walks * n                      # walks per rank per step
+    out = torch.empty((B, L), dtype=torch.int32, device=dev)
+    cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+    gather = None
+    if args.allgather and world > 1:
+        gather = torch.empty((world * B, L), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = C.ctypes.c_void_p(stream.cuda_stream)
+
+    def step(i, events=None):
+        # global walk index block of (rank, step i): iterations
+        # num_walks*(i*world+rank) ... +num_walks-1 of the reference loop
+        w0 = (i * world + rank) * B
+        if events is not None:
+            events[0].record(stream)
+        C.check(C.lib().gw_n2v_walks(G.handle, L, args.seed, w0, B, 1, C.ptr(out), None, C.ptr(cnt), sh),
+                G.handle)
+        if events is not None:
+            events[1].record(stream)
+        if gather is not None:
+            dist.all_gather_into_tensor(gather, out)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    cnt.zero_()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    steps_local = int(cnt[0].item())
+    trials_local = int(cnt[1].item())
+    kms = [a.elapsed_time(b) for a, b in evs]
+    k_avg_ms = sum(kms) / len(kms)
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        s = torch.tensor([steps_local, trials_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        steps_total, trials_total = int(s[0].item()), int(s[1].item())
+    else:
+        steps_total, trials_total = steps_local, trials_local
+    value = steps_total / el
+    launch_steps = steps_local // args.steps
+    achieved = BYTES_PER_STEP * launch_steps / (k_avg_ms * 1e-3) / 1e9
+    tag = f"n2v_rmat{args.scale}_p{args.p}_q{args.q}_L{L}_r{args.num_walks}"
+    traffic = load_traffic(tag, launch_steps)
+
+    # ---- parity spot check (cheap): every step follows an edge ----
+    if rank == 0:
+        csr = G.export_csr()
+        smp = out[:2000].cpu().numpy()
+        offs, nbrs = csr["offsets"], csr["nbrs"]
+        a, b = smp[:, :-1].ravel(), smp[:, 1:].ravel()
+        pos = np.array([np.searchsorted(nbrs[offs[x]:offs[x + 1]], y) for x, y in zip(a, b)])
+        ok = all(nbrs[offs[x] + p] == y for x, y, p in zip(a, b, pos))
+        if not ok:
+            log("PARITY SPOT CHECK FAILED: a step does not follow an edge")
+            sys.exit(3)
+
+    # ---- TopSim secondary metric (config 3: lshrank blog) ----
+    secondary = None
+    if not args.no_topsim:
+        from gwamd import topsim
+        data = os.path.join(ROOT, "tests", "golden", "data", "blog.txt")
+        tg = topsim.Graph(data, 10313, separator=",", device=dev.index)
+        tg._ensure_device()
+        src = torch.arange(10313, dtype=torch.int32, device=dev)
+        K = 20
+        ids = torch.empty((10313, K), dtype=torch.int32, device=dev)
+        sc = torch.empty((10313, K), dtype=torch.float64, device=dev)
+        st = torch.zeros(4, dtype=torch.int64, device=dev)
+        h = tg._g.handle
+
+        def ts_run(stats_ptr):
+            C.check(C.lib().gw_topsim(h, C.TOPSIM_SINGLE_SAMPLE, args.topsim_sample, args.topsim_step, 0.6,
+                                      args.seed, C.ptr(src), 10313, K, C.ptr(ids), C.ptr(sc), stats_ptr, sh), h)
+
+        ts_run(None)  # warm-up (also sizes the workspace)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t1 = time.perf_counter()
+        e0.record(stream)
+        ts_run(C.ptr(st))
+        e1.record(stream)
+        torch.cuda.synchronize()
+        tel = time.perf_counter() - t1
+        kt = e0.elapsed_time(e1) * 1e-3
+        if world > 1:
+            t = torch.tensor([tel], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            tel = float(t.item())
+            dist.all_reduce(st, op=dist.ReduceOp.SUM)
+        ext, upd = int(st[0].item()), int(st[1].item())
+        alg = (TOPSIM_B_EXT * ext + TOPSIM_B_UPD * upd) / max(world, 1)
+        secondary = {
+            "metric": "SimRank pair-updates/sec (TopSim_singleSample)", "value": upd / tel,
+            "unit": "pair-updates/s", "path_extensions_per_s": ext / tel,
+            "config": {"workload": "TopSim_singleSample on lshrank blog (V=10313, 333,983 edges, Java "
+                                   "multigraph), all sources, replicated per rank",
+                       "step": args.topsim_step, "sample": args.topsim_sample, "C": 0.6, "topk": K},
+            "pair_updates": upd, "path_extensions": ext, "seconds": tel,
+            "roofline": {"bound": "hbm", "achieved": alg / kt / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / kt / 1e9 / HBM_PEAK_GBS, "traffic": None},
+        }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(G.export_csr(), args, 0)
+
+    if rank == 0:
+        res = {
+            "metric": "walk-steps/sec (node2vec)",
+            "value": value,
+            "unit": "walk-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32 ids / f64 accept tests",
+            "data": "synthetic",
+            "config": {"workload": f"node2vec p={args.p} q={args.q} on synthetic Graph500 R-MAT scale-{args.scale} "
+                                   f"(ef {args.edge_factor}, a,b,c=0.57,0.19,0.19, seed {args.seed}; n={n}, "
+                                   f"adjacency entries={nnz}), walk_length={L}, {args.num_walks} walks/node per "
+                                   f"rank per step",
+                       "global_batch": B * world, "seq_len": L, "parallelism": f"dp{world}",
+                       "allgather": bool(gather is not None)},
+            "walk_steps": steps_total,
+            "rejection_trials_per_step": trials_total / max(steps_total, 1),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_walk_scale<false,false,false>", "kernel_ms": k_avg_ms,
+                         "bytes_per_unit": BYTES_PER_STEP, "units_per_launch": launch_steps},
+            "cpu_baseline": cpu,
+            "secondary": secondary,
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

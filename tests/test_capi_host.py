@@ -1,0 +1,179 @@
+"""CPU: the C-ABI library loads, exports every declared symbol, and its host
+logic (graph semantics, generators, writers) matches the reference formats.
+No compute (GPU) calls are made here."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import DATA, ROOT, golden_index, load_golden
+
+CASES = golden_index()["cases"]
+
+
+def test_exports_every_declared_symbol(gw):
+    with open(os.path.join(ROOT, "include", "graphwalk.h")) as f:
+        hdr = f.read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    declared = sorted(set(re.findall(r"\b(gw_[a-z0-9_]+)\s*\(", hdr)))
+    assert len(declared) >= 20
+    L = gw.lib()
+    for name in declared:
+        assert hasattr(L, name), name
+    from gwamd._lib import SIGNATURES
+    assert sorted(SIGNATURES) == declared
+
+
+def test_version_and_errors(gw):
+    L = gw.lib()
+    assert b"gfx950" in L.gw_version()
+    assert L.gw_strerror(-11) == b"capacity exceeded"
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c["file"])
+def test_nx_loader_matches_networkx(case, gw):
+    """gw_graph_load_edgelist(NX_SIMPLE) == read_graph (main.py:76-89) as
+    networkx built it when the goldens were generated."""
+    g = load_golden(case["file"])
+    G = gw.GWGraph.from_edgelist(os.path.join(DATA, case["graph"]), delimiter=case["delimiter"],
+                                 semantics="nx", directed=case["directed"], weighted=case["weighted"])
+    c = G.export_csr()
+    np.testing.assert_array_equal(c["labels"], g["labels"])
+    np.testing.assert_array_equal(c["offsets"], g["offsets"])
+    np.testing.assert_array_equal(c["labels"][c["nbrs"]], g["nbrs"])
+    np.testing.assert_array_equal(c["weights"], g["weights"])
+    np.testing.assert_array_equal(c["labels"][c["node_order"]], g["node_order"])
+    assert G.info().device == -1
+
+
+def test_from_networkx_matches_loader(gw):
+    import networkx as nx
+    path = os.path.join(DATA, "weighted_quirks.edgelist")
+    G = nx.read_edgelist(path, nodetype=int, data=(("weight", float),), create_using=nx.DiGraph(),
+                         delimiter=" ").to_undirected()
+    a = gw.GWGraph.from_networkx(G).export_csr()
+    b = gw.GWGraph.from_edgelist(path, " ", "nx", False, True).export_csr()
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k])
+
+
+@pytest.mark.parametrize("fname,V,sep", [("moreno_crime_crime.txt", 1380, "\t"),
+                                         ("blog.txt", 10313, ","), ("0_333_5038.txt", 333, " ")])
+def test_java_loader(fname, V, sep, gw):
+    """gw_graph_load_edgelist(JAVA_MULTI) == structures.Graph (Graph.java:28-57)."""
+    adj = [[] for _ in range(V)]
+    with open(os.path.join(DATA, fname)) as f:
+        for line in f:
+            a, b = line.rstrip("\r\n").split(sep)[:2]
+            adj[int(a)].append(int(b))
+            adj[int(b)].append(int(a))
+    c = gw.GWGraph.from_edgelist(os.path.join(DATA, fname), delimiter=sep, semantics="java",
+                                 vcount=V).export_csr()
+    np.testing.assert_array_equal(np.diff(c["offsets"]), [len(x) for x in adj])
+    np.testing.assert_array_equal(c["nbrs"], [y for x in adj for y in x])
+
+
+def test_java_loader_errors(gw, tmp_path):
+    p = tmp_path / "bad.txt"
+    p.write_text("0,1\n2,7\n")
+    with pytest.raises(IndexError):  # ArrayIndexOutOfBounds: id >= V
+        gw.GWGraph.from_edgelist(str(p), ",", "java", vcount=5)
+    p.write_text("0\t1\n")
+    with pytest.raises(ValueError):  # shipped SEPARATOR "," cannot parse tab files
+        gw.GWGraph.from_edgelist(str(p), ",", "java", vcount=5)
+    p.write_text("0,1\n\n1,2\n")
+    with pytest.raises(ValueError):  # blank line -> ids[1] out of bounds in Java
+        gw.GWGraph.from_edgelist(str(p), ",", "java", vcount=5)
+
+
+def test_nx_loader_quirks(gw, tmp_path):
+    p = tmp_path / "e.txt"
+    # comments, blank lines, '\r', trailing-delimiter error
+    p.write_text("# header\n5 7\n\n7 9 # c\n")
+    with pytest.raises(ValueError):  # "7 9 " -> extra empty data token (networkx TypeError)
+        gw.GWGraph.from_edgelist(str(p), " ", "nx")
+    p.write_text("# header\n5 7\r\n\n7 9\n9 5\n")
+    c = gw.GWGraph.from_edgelist(str(p), " ", "nx").export_csr()
+    np.testing.assert_array_equal(c["labels"], [5, 7, 9])
+    np.testing.assert_array_equal(c["offsets"], [0, 2, 4, 6])
+    # default delimiter ',' on a space file parses zero edges
+    c = gw.GWGraph.from_edgelist(os.path.join(DATA, "karate.edgelist"), ",", "nx").export_csr()
+    assert len(c["labels"]) == 0
+
+
+def test_rmat_generator(gw):
+    G = gw.GWGraph.rmat(12, 16, seed=42)
+    c = G.export_csr()
+    n = len(c["labels"])
+    offs, nbrs = c["offsets"], c["nbrs"]
+    deg = np.diff(offs)
+    assert deg.min() >= 1  # isolated vertices removed
+    rows = np.repeat(np.arange(n), deg)
+    assert not np.any(rows == nbrs)  # no self loops
+    for v in range(0, n, 97):
+        r = nbrs[offs[v]:offs[v + 1]]
+        assert np.all(np.diff(r) > 0)  # sorted, deduplicated
+    key = set(zip(rows.tolist(), nbrs.tolist()))
+    assert all((b, a) in key for (a, b) in list(key)[:5000])  # symmetric
+    c2 = gw.GWGraph.rmat(12, 16, seed=42).export_csr()
+    np.testing.assert_array_equal(c2["nbrs"], nbrs)  # deterministic
+    c3 = gw.GWGraph.rmat(12, 16, seed=43).export_csr()
+    assert len(c3["nbrs"]) != len(nbrs) or not np.array_equal(c3["nbrs"], nbrs)
+
+
+def test_walk_writer_format(gw, tmp_path):
+    """DeepSim save_list (DeepSim/src/main.py:237-243): 'id\\t' per id."""
+    from gwamd import io
+    G = gw.GWGraph.from_edgelist(os.path.join(DATA, "karate.edgelist"), " ", "nx")
+    lab = G.export_csr()["labels"]
+    walks = np.array([[0, 1, 2, -1], [3, 3, 4, 5]], np.int32)
+    p1 = tmp_path / "a.txt"
+    p2 = tmp_path / "b.txt"
+    io.save_walks(G, p1, walks)
+    io.save_list([[int(lab[0]), int(lab[1]), int(lab[2])], [int(lab[i]) for i in (3, 3, 4, 5)]], p2)
+    assert p1.read_bytes() == p2.read_bytes()
+    assert io.read_list(p1)[1] == [str(int(lab[i])) for i in (3, 3, 4, 5)]
+
+
+def test_sim_writer_java_exact(gw, oracle, tmp_path):
+    """Print.printByOrder (Print.java:25-53): FixedMaxPQ tie order and Java
+    %.6f HALF_UP, CRLF line ends."""
+    from gwamd import topsim
+    rng = np.random.RandomState(0)
+    rows = np.round(rng.rand(40, 57) * 8) / 8  # many ties
+    rows[3] = 0.0
+    rows[5, :5] = 1.0000005
+    out = tmp_path / "s.txt"
+    topsim.printByOrder(rows, str(out), topk=20)
+    lines = open(str(out) + ".sim.txt", "rb").read().split(b"\r\n")
+    ids_lines = open(out, "rb").read().split(b"\r\n")
+    for v in range(40):
+        exp = oracle.java_fixed_max_pq_row(rows[v], 20)
+        s = f"{v}" + "".join(f",{i}:{oracle.java_format_fixed(x)}" for i, x in exp)
+        assert lines[v].decode() == s
+        assert ids_lines[v].decode() == f"{v}" + "".join(f",{i}" for i, _ in exp)
+
+
+def test_precision_metric(tmp_path):
+    """Eval.precision (Eval.java:81-131)."""
+    from gwamd import topsim
+    g = tmp_path / "g.sim.txt"
+    t = tmp_path / "t.sim.txt"
+    g.write_text("0,1:0.5,2:0.4,3:0.0\r\n1,0:0.0\r\n")
+    t.write_text("0,2:0.9,5:0.3\r\n1,4:0.2\r\n")
+    pre = topsim.precision(str(g), str(t), str(tmp_path / "p.txt"), 20)
+    assert pre == pytest.approx((0.5 + 1.0) / 2)
+
+
+def test_compute_calls_fail_loudly_without_gpu(gw):
+    """No CPU fallback: on a host without a GPU the device calls raise."""
+    from gwamd._lib import DeviceError
+    if gw.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    G = gw.GWGraph.from_edgelist(os.path.join(DATA, "karate.edgelist"), " ", "nx")
+    with pytest.raises(DeviceError):
+        G.to_device(0)
+    with pytest.raises(Exception):
+        from gwamd.node2vec import alias_setup
+        alias_setup([0.5, 0.5])

@@ -1,0 +1,196 @@
+"""GPU parity for node2vec (H1): the HIP kernels behind the C ABI against the
+reference goldens (exact replay) and against the oracle (Philox scale mode)."""
+import hashlib
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import DATA, golden_index, load_golden
+
+pytestmark = pytest.mark.gpu
+CASES = golden_index()["cases"]
+
+
+def _nx_graph(case):
+    import networkx as nx
+    path = os.path.join(DATA, case["graph"])
+    if case["weighted"]:
+        G = nx.read_edgelist(path, nodetype=int, data=(("weight", float),), create_using=nx.DiGraph(),
+                             delimiter=case["delimiter"])
+    else:
+        G = nx.read_edgelist(path, nodetype=int, create_using=nx.DiGraph(), delimiter=case["delimiter"])
+        for e in G.edges():
+            G[e[0]][e[1]]["weight"] = 1
+    if not case["directed"]:
+        G = G.to_undirected()
+    return G
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c["file"])
+def test_replay_mirror_matches_reference(case, gw):
+    """gwamd.node2vec.Graph (drop-in for node2vec.Graph) reproduces the
+    reference walks bit-for-bit from the same seeds, and advances the global
+    RNG states exactly as the reference does."""
+    from gwamd import node2vec
+    g = load_golden(case["file"])
+    G = _nx_graph(case)
+    random.seed(case["seed"])
+    np.random.seed(case["seed"])
+    n2v = node2vec.Graph(G, case["directed"], case["p"], case["q"])
+    n2v.preprocess_transition_probs()
+    walks = n2v.simulate_walks(case["num_walks"], case["walk_length"])
+    L = case["walk_length"]
+    W = np.full((len(walks), L), -1, np.int64)
+    for i, w in enumerate(walks):
+        W[i, :len(w)] = w
+    assert hashlib.sha256(W.tobytes()).hexdigest() == case["walks_sha256"]
+    if case["full_walks"]:
+        np.testing.assert_array_equal(W, g["walks"])
+    # global stream advanced by exactly 2 uniforms per step
+    ref = np.random.RandomState(case["seed"])
+    ref.random_sample(2 * int((g["lens"] - 1).sum()))
+    assert np.random.random_sample() == ref.random_sample()
+    # alias tables exposed like the reference dicts
+    lab = g["labels"]
+    u = int(lab[0])
+    J, q = n2v.alias_nodes[u]
+    b, e = g["offsets"][0], g["offsets"][1]
+    np.testing.assert_array_equal(J, g["alias_node_J"][b:e])
+    assert q.tobytes() == g["alias_node_q"][b:e].tobytes()
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["full_walks"]], ids=lambda c: c["file"])
+def test_gpu_alias_tables_bitwise(case, gw):
+    """k_alias_nodes / k_alias_edges == reference alias tables, bitwise."""
+    from gwamd import _lib as C
+    g = load_golden(case["file"])
+    G = gw.GWGraph.from_edgelist(os.path.join(DATA, case["graph"]), case["delimiter"], "nx",
+                                 case["directed"], case["weighted"]).to_device(0)
+    C.check(C.lib().gw_n2v_prepare(G.handle, float(case["p"]), float(case["q"]), C.N2V_REPLAY), G.handle)
+    inf = G.info()
+    nJ = np.empty(inf.nnz, np.int32)
+    nq = np.empty(inf.nnz, np.float64)
+    eoff = np.empty(inf.nnz + 1, np.int64)
+    eJ = np.empty(inf.edge_alias_entries, np.int32)
+    eq = np.empty(inf.edge_alias_entries, np.float64)
+    C.check(C.lib().gw_n2v_export_alias(G.handle, C.ptr(nJ), C.ptr(nq), C.ptr(eoff), C.ptr(eJ), C.ptr(eq)),
+            G.handle)
+    np.testing.assert_array_equal(nJ, g["alias_node_J"])
+    assert nq.tobytes() == g["alias_node_q"].tobytes()
+    np.testing.assert_array_equal(eoff, g["alias_edge_off"])
+    np.testing.assert_array_equal(eJ, g["alias_edge_J"])
+    assert eq.tobytes() == g["alias_edge_q"].tobytes()
+
+
+def test_alias_setup_standalone(gw, oracle):
+    from gwamd.node2vec import alias_setup
+    rng = np.random.RandomState(5)
+    for K in (1, 2, 3, 7, 49, 1000):
+        p = rng.rand(K)
+        p /= p.sum()
+        J, q = alias_setup(p)
+        J2, q2 = oracle.alias_setup(p)
+        np.testing.assert_array_equal(J, J2)
+        assert q.tobytes() == q2.tobytes()
+
+
+def _scale_case(gw, oracle, path, delim, directed, weighted, p, q, seed, L, begin, count, shuffle=True):
+    import torch
+    from gwamd import _lib as C
+    G = gw.GWGraph.from_edgelist(path, delim, "nx", directed, weighted).to_device(0)
+    C.check(C.lib().gw_n2v_prepare(G.handle, float(p), float(q), C.N2V_REJECTION), G.handle)
+    out = torch.empty((count, L), dtype=torch.int32, device="cuda")
+    lens = torch.empty(count, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    C.check(C.lib().gw_n2v_walks(G.handle, L, seed, begin, count, int(shuffle), C.ptr(out), C.ptr(lens),
+                                 C.ptr(cnt), None), G.handle)
+    torch.cuda.synchronize()
+    csr = G.export_csr()
+    o2, l2, c2 = oracle.walks_scale(csr if weighted else dict(csr, weights=None), p, q, seed, L, begin,
+                                    count, shuffle=shuffle, directed=directed, nthreads=8)
+    np.testing.assert_array_equal(out.cpu().numpy(), o2)
+    np.testing.assert_array_equal(lens.cpu().numpy(), l2)
+    assert int(cnt[0]) == int(c2[0]) and int(cnt[1]) == int(c2[1])
+    return out.cpu().numpy(), csr
+
+
+@pytest.mark.parametrize("p,q", [(1, 1), (0.25, 4), (1, 0.5), (4, 0.25), (2, 1)])
+@pytest.mark.parametrize("graph,delim", [("karate.edgelist", " "), ("moreno_crime_crime.txt", "\t"),
+                                         ("arxiv_author_pub.txt", "\t")])
+def test_scale_walks_gpu_equals_oracle(gw, oracle, graph, delim, p, q):
+    n = {"karate.edgelist": 34, "moreno_crime_crime.txt": 1380, "arxiv_author_pub.txt": 38741}[graph]
+    count = min(3 * n, 50000)
+    _scale_case(gw, oracle, os.path.join(DATA, graph), delim, False, False, p, q, 1234, 40, n // 3, count)
+
+
+@pytest.mark.parametrize("directed,weighted,graph", [(True, False, "directed_sinks.edgelist"),
+                                                     (False, True, "weighted_quirks.edgelist")])
+def test_scale_walks_directed_weighted(gw, oracle, directed, weighted, graph):
+    for (p, q) in [(1, 1), (0.5, 2), (0.25, 4)]:
+        _scale_case(gw, oracle, os.path.join(DATA, graph), " ", directed, weighted, p, q, 99, 25, 0, 500)
+
+
+def test_scale_walks_shard_invariance_and_properties(gw, oracle):
+    """Output is a pure function of the global walk index: any shard split
+    gives the same walks; every step follows an edge; each iteration starts
+    every vertex exactly once (per-iteration keyed permutation)."""
+    import torch
+    from gwamd import _lib as C
+    G = gw.GWGraph.rmat(14, 16, seed=7).to_device(0)
+    C.check(C.lib().gw_n2v_prepare(G.handle, 0.25, 4.0, C.N2V_REJECTION), G.handle)
+    n = G.n
+    L = 20
+    tot = 2 * n
+    full = torch.empty((tot, L), dtype=torch.int32, device="cuda")
+    C.check(C.lib().gw_n2v_walks(G.handle, L, 5, 0, tot, 1, C.ptr(full), None, None, None), G.handle)
+    parts = []
+    for b, e in [(0, 777), (777, n + 5), (n + 5, tot)]:
+        t = torch.empty((e - b, L), dtype=torch.int32, device="cuda")
+        C.check(C.lib().gw_n2v_walks(G.handle, L, 5, b, e - b, 1, C.ptr(t), None, None, None), G.handle)
+        parts.append(t)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(torch.cat(parts).cpu().numpy(), full.cpu().numpy())
+    W = full.cpu().numpy()
+    csr = G.export_csr()
+    offs, nbrs = csr["offsets"], csr["nbrs"]
+    for it in range(2):
+        starts = np.sort(W[it * n:(it + 1) * n, 0])
+        np.testing.assert_array_equal(starts, np.arange(n))
+    a, b = W[:, :-1].ravel(), W[:, 1:].ravel()
+    ok = np.array([np.searchsorted(nbrs[offs[x]:offs[x + 1]], y) < offs[x + 1] - offs[x] and
+                   nbrs[offs[x] + np.searchsorted(nbrs[offs[x]:offs[x + 1]], y)] == y
+                   for x, y in zip(a[:20000], b[:20000])])
+    assert ok.all()
+    # oracle parity on a random window
+    o2, _, _ = oracle.walks_scale(dict(csr, weights=None), 0.25, 4.0, 5, L, 1000, 3000, nthreads=8)
+    np.testing.assert_array_equal(W[1000:4000], o2)
+
+
+def test_replay_capi_from_loader(gw, oracle):
+    """C-ABI replay path on the C++-parsed graph == oracle replay."""
+    from gwamd import _lib as C
+    case = [c for c in CASES if c["file"].startswith("n2v_moreno")][0]
+    g = load_golden(case["file"])
+    G = gw.GWGraph.from_edgelist(os.path.join(DATA, case["graph"]), "\t", "nx").to_device(0)
+    C.check(C.lib().gw_n2v_prepare(G.handle, case["p"], case["q"], C.N2V_REPLAY), G.handle)
+    csr = G.export_csr()
+    rank = {int(x): i for i, x in enumerate(csr["labels"])}
+    starts = np.array([rank[int(x)] for x in g["starts"]], np.int32)
+    L = case["walk_length"]
+    U = np.random.RandomState(case["seed"]).random_sample(2 * (L - 1) * len(starts))
+    out = np.empty((len(starts), L), np.int32)
+    lens = np.empty(len(starts), np.int32)
+    used = C.I64(0)
+    C.check(C.lib().gw_n2v_walks_replay(G.handle, L, len(starts), C.ptr(starts), C.ptr(U), len(U), C.ptr(out),
+                                        C.ptr(lens), C.ctypes.byref(used)), G.handle)
+    np.testing.assert_array_equal(csr["labels"][out], g["walks"])
+    assert used.value == 2 * int((g["lens"] - 1).sum())
+
+
+def test_replay_refuses_huge_edge_tables(gw):
+    from gwamd import _lib as C
+    G = gw.GWGraph.rmat(18, 16, seed=1).to_device(0)
+    with pytest.raises(C.CapacityError):
+        C.check(C.lib().gw_n2v_prepare(G.handle, 0.25, 4.0, C.N2V_REPLAY), G.handle)
