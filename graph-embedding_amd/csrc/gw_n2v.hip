@@ -655,3 +655,36 @@ extern "C" int gw_n2v_export_alias(const gw_graph* gc, int32_t* node_J, double* 
   }
   return GW_OK;
 }
+
+extern "C" int gw_n2v_walks_host(gw_graph* g, int walk_len, uint64_t seed, int64_t walk_begin,
+                                 int64_t walk_count, int shuffle, int32_t* out_walks, int32_t* out_len,
+                                 uint64_t* counters) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  if (!g->n2v_prepared) return gw_fail(g, GW_ERR_STATE, "call gw_n2v_prepare first");
+  if (walk_len < 1 || walk_begin < 0 || walk_count < 0 || (walk_count > 0 && !out_walks))
+    return gw_fail(g, GW_ERR_INVALID, "bad arguments");
+  if (walk_count == 0) return GW_OK;
+  GW_HIP_TRY(hipSetDevice(g->device));
+  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(walk_count, ((int64_t)1 << 30) / (4 * (int64_t)walk_len)));
+  int32_t *d_out = nullptr, *d_len = nullptr;
+  uint64_t* d_cnt = nullptr;
+  int rc;
+  if ((rc = dev_alloc(g, &d_out, chunk * (int64_t)walk_len)) || (rc = dev_alloc(g, &d_len, chunk)) ||
+      (rc = dev_alloc(g, &d_cnt, 2))) {
+    dev_free(d_out); dev_free(d_len); dev_free(d_cnt);
+    return rc;
+  }
+  hipError_t e = hipMemset(d_cnt, 0, 2 * sizeof(uint64_t));
+  for (int64_t c0 = 0; c0 < walk_count && e == hipSuccess; c0 += chunk) {
+    const int64_t cn = std::min(chunk, walk_count - c0);
+    rc = gw_dev_n2v_walks(g, walk_len, seed, walk_begin + c0, cn, shuffle, d_out, d_len, d_cnt, nullptr);
+    if (rc != GW_OK) break;
+    e = hipMemcpy(out_walks + c0 * walk_len, d_out, cn * walk_len * sizeof(int32_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && out_len) e = hipMemcpy(out_len + c0, d_len, cn * sizeof(int32_t), hipMemcpyDeviceToHost);
+  }
+  if (rc == GW_OK && e == hipSuccess && counters) e = hipMemcpy(counters, d_cnt, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  dev_free(d_out); dev_free(d_len); dev_free(d_cnt);
+  if (rc != GW_OK) return rc;
+  if (e != hipSuccess) return gw_fail(g, GW_ERR_DEVICE, "%s", hipGetErrorString(e));
+  return GW_OK;
+}

@@ -759,3 +759,54 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   }
   return GW_OK;
 }
+
+// ---------------------------------------------------------------------------
+// host-buffer conveniences (JNI shim / C++ host / CLI): stage through HBM
+// ---------------------------------------------------------------------------
+extern "C" int gw_topsim_host(gw_graph* g, int variant, int sample, int step, double C, uint64_t seed,
+                              const int32_t* sources, int64_t nsrc, int topk, int32_t* out_ids,
+                              double* out_scores, double* out_rows, int64_t* stats) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  if (g->device < 0) return gw_fail(g, GW_ERR_STATE, "graph is not on a device");
+  if (nsrc < 0 || (nsrc > 0 && !sources) || (!out_rows && (!out_ids || !out_scores)) || topk < 0)
+    return gw_fail(g, GW_ERR_INVALID, "bad arguments");
+  for (int64_t i = 0; i < nsrc; ++i)
+    if (sources[i] < 0 || sources[i] >= g->n) return gw_fail(g, GW_ERR_RANGE, "source %d out of [0,V)", sources[i]);
+  GW_HIP_TRY(hipSetDevice(g->device));
+  const int64_t n = g->n;
+  // chunk so the staging buffers stay under ~1 GB
+  const int64_t row_bytes = out_rows ? n * 8 : (int64_t)topk * 12;
+  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(nsrc, ((int64_t)1 << 30) / std::max<int64_t>(row_bytes, 1)));
+  int32_t* d_src = nullptr;
+  int32_t* d_ids = nullptr;
+  double* d_sc = nullptr;
+  double* d_rows = nullptr;
+  int64_t* d_st = nullptr;
+  int rc = GW_OK;
+  if ((rc = ws_alloc(g, &d_src, chunk)) || (rc = ws_alloc(g, &d_st, 4)) ||
+      (out_rows ? (rc = ws_alloc(g, &d_rows, chunk * n)) : ((rc = ws_alloc(g, &d_ids, chunk * (int64_t)std::max(topk, 1))) ||
+                                                            (rc = ws_alloc(g, &d_sc, chunk * (int64_t)std::max(topk, 1)))))) {
+    ws_free(d_src); ws_free(d_st); ws_free(d_rows); ws_free(d_ids); ws_free(d_sc);
+    return rc;
+  }
+  hipError_t e = hipMemset(d_st, 0, 4 * sizeof(int64_t));
+  for (int64_t c0 = 0; c0 < nsrc && rc == GW_OK && e == hipSuccess; c0 += chunk) {
+    const int64_t cn = std::min(chunk, nsrc - c0);
+    e = hipMemcpy(d_src, sources + c0, cn * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) break;
+    rc = gw_dev_topsim(g, variant, sample, step, C, seed, d_src, cn, out_rows ? 0 : topk, out_rows ? nullptr : d_ids,
+                       out_rows ? nullptr : d_sc, d_rows, d_st, nullptr);
+    if (rc != GW_OK) break;
+    if (out_rows) {
+      e = hipMemcpy(out_rows + c0 * n, d_rows, cn * n * sizeof(double), hipMemcpyDeviceToHost);
+    } else {
+      e = hipMemcpy(out_ids + c0 * topk, d_ids, cn * topk * sizeof(int32_t), hipMemcpyDeviceToHost);
+      if (e == hipSuccess) e = hipMemcpy(out_scores + c0 * topk, d_sc, cn * topk * sizeof(double), hipMemcpyDeviceToHost);
+    }
+  }
+  if (rc == GW_OK && e == hipSuccess && stats) e = hipMemcpy(stats, d_st, 4 * sizeof(int64_t), hipMemcpyDeviceToHost);
+  ws_free(d_src); ws_free(d_st); ws_free(d_rows); ws_free(d_ids); ws_free(d_sc);
+  if (rc != GW_OK) return rc;
+  if (e != hipSuccess) return gw_fail(g, GW_ERR_DEVICE, "%s", hipGetErrorString(e));
+  return GW_OK;
+}

@@ -100,7 +100,10 @@ SIGNATURES = {
     "gw_alias_setup": (ctypes.c_int, [ctypes.c_int, P, I64, P, P]),
     "gw_n2v_walks_replay": (ctypes.c_int, [P, ctypes.c_int, I64, P, P, I64, P, P, PI64]),
     "gw_n2v_walks": (ctypes.c_int, [P, ctypes.c_int, U64, I64, I64, ctypes.c_int, P, P, P, P]),
-    "gw_topsim_prepare": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "gw_n2v_walks_host": (ctypes.c_int, [P, ctypes.c_int, U64, I64, I64, ctypes.c_int, P, P, P]),
+    "gw_topsim_host": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, U64, P, I64,
+                                      ctypes.c_int, P, P, P, P]),
+    "gw_topsim_prepare":(ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "gw_topsim": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, U64, P, I64,
                                  ctypes.c_int, P, P, P, P]),
     "gw_topsim_dense": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, U64, P, I64,

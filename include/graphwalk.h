@@ -177,6 +177,13 @@ int gw_n2v_walks(gw_graph* g, int walk_len, uint64_t seed, int64_t walk_begin,
                  int64_t walk_count, int shuffle, int32_t* out_walks_dev,
                  int32_t* out_len_dev, uint64_t* counters_dev, void* stream);
 
+/* Host-buffer form of gw_n2v_walks (stages through HBM in ~1 GB chunks and
+ * synchronises): out_walks[walk_count*walk_len], out_len[walk_count] (NULL
+ * ok), counters[2] (NULL ok).  For JNI / CLI callers.                       */
+int gw_n2v_walks_host(gw_graph* g, int walk_len, uint64_t seed,
+                      int64_t walk_begin, int64_t walk_count, int shuffle,
+                      int32_t* out_walks, int32_t* out_len, uint64_t* counters);
+
 /* ---- TopSim (H2) ------------------------------------------------------------ */
 /* Allocate the per-workgroup workspace for up to `sample`/`step` (kept in the
  * handle; sizes the level arrays and the accumulator rows).                 */
@@ -198,6 +205,14 @@ int gw_topsim(gw_graph* g, int variant, int sample, int step, double C,
 int gw_topsim_dense(gw_graph* g, int variant, int sample, int step, double C,
                     uint64_t seed, const int32_t* sources_dev, int64_t nsrc,
                     double* out_rows_dev, int64_t* stats_dev, void* stream);
+
+/* Host-buffer form of gw_topsim / gw_topsim_dense for JNI and C++ callers:
+ * sources[nsrc] on the host; either out_rows[nsrc*n] (dense, getResult())
+ * or out_ids/out_scores[nsrc*topk] (top-k); stats[4] optional.            */
+int gw_topsim_host(gw_graph* g, int variant, int sample, int step, double C,
+                   uint64_t seed, const int32_t* sources, int64_t nsrc,
+                   int topk, int32_t* out_ids, double* out_scores,
+                   double* out_rows, int64_t* stats);
 
 /* ---- output writers (host) ------------------------------------------------ */
 /* DeepSim save_list format (DeepSim/src/main.py:237-243): one walk per line,

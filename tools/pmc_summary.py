@@ -1,0 +1,64 @@
+"""Summarise rocprofv3 PMC passes into profiles/pmc_summary.json.
+
+    python tools/pmc_summary.py TAG FETCH_CSV WRITE_CSV BENCH_JSON
+
+HBM traffic per launch = (FETCH_SIZE + WRITE_SIZE) * 1024 bytes, averaged
+over the dispatches of the kernel (MI355X_MICROARCH.md §HBM: both counters
+are in KiB, read from TCC_EA0 memory-side requests; Infinity-Cache hits are
+counted).  The gfx950 x2 correction for FETCH_SIZE applies to wide (16 B per
+lane) coalesced streaming reads only; the walk kernel's reads are random 4-8 B
+gathers (one 64 B request per missing line), so FETCH_SIZE is used as is and
+the summary says so.
+"""
+import csv
+import json
+import os
+import sys
+
+
+def per_kernel(path, counter):
+    acc = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        k = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+        acc.setdefault(k, []).append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    tag, fcsv, wcsv, bjson = sys.argv[1:5]
+    f = per_kernel(fcsv, "FETCH_SIZE")
+    w = per_kernel(wcsv, "WRITE_SIZE")
+    bench = json.load(open(bjson))
+    out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                            "pmc_summary.json")
+    try:
+        summ = json.load(open(out_path))
+    except Exception:
+        summ = {}
+    roof = bench["roofline"]
+    walk_key = [k for k in f if k.startswith("k_walk_scale")][0]
+    fb, wb = f[walk_key] * 1024, w[walk_key] * 1024
+    summ[tag] = {
+        "kernel": walk_key,
+        "walk_steps_per_launch": roof["units_per_launch"],
+        "fetch_bytes_per_launch": fb,
+        "write_bytes_per_launch": wb,
+        "hbm_bytes_per_launch": fb + wb,
+        "algorithmic_bytes_per_launch": roof["bytes_per_unit"] * roof["units_per_launch"],
+        "fetch_bytes_per_step": fb / roof["units_per_launch"],
+        "write_bytes_per_step": wb / roof["units_per_launch"],
+        "note": "FETCH_SIZE/WRITE_SIZE (KiB) x 1024, mean over dispatches, separate --pmc passes; "
+                "FETCH_SIZE not doubled (random gathers, not 16 B/lane streaming)",
+    }
+    ts = [k for k in f if k.startswith("k_topsim")]
+    if ts and bench.get("secondary"):
+        summ[tag]["topsim"] = {"kernel": ts[0], "fetch_bytes_per_launch": f[ts[0]] * 1024,
+                               "write_bytes_per_launch": w[ts[0]] * 1024}
+    json.dump(summ, open(out_path, "w"), indent=1)
+    print(json.dumps(summ[tag], indent=1))
+
+
+if __name__ == "__main__":
+    main()
