@@ -127,6 +127,7 @@ def main():
 
     import gwamd
     from gwamd import _lib as C
+    from gwamd import dist as gdist
     L = args.walk_length
 
     # ---- graph (host build, replicated on every rank) ----
@@ -151,7 +152,7 @@ def main():
     def step(i, events=None):
         # global walk index block of (rank, step i): iterations
         # num_walks*(i*world+rank) ... +num_walks-1 of the reference loop
-        w0 = (i * world + rank) * B
+        w0 = gdist.weak_block(i, world, rank, B)
         if events is not None:
             events[0].record(stream)
         C.check(C.lib().gw_n2v_walks(G.handle, L, args.seed, w0, B, 1, C.ptr(out), None, C.ptr(cnt), sh),

@@ -19,6 +19,7 @@
 //   deg      int32[n]     row lengths (TopSim reads deg(mid), deg(target))
 //   node_J/q int32/f64[nnz] per-node alias tables (weighted or REPLAY)
 //   edge_off int64[nnz+1], edge_J/q per-edge alias tables (REPLAY only)
+//   bitmap   u32[16*nnz/32] has_edge membership pre-filter (REJECTION, p/q != 1)
 struct gw_dev_graph {
   int64_t n = 0, nnz = 0;
   int64_t* offsets = nullptr;
@@ -32,6 +33,7 @@ struct gw_dev_graph {
   int64_t* edge_off = nullptr;
   int32_t* edge_J = nullptr;
   double* edge_q = nullptr;
+  uint32_t* bitmap = nullptr;  // has_edge pre-filter, 16 bits per entry
 };
 
 struct gw_topsim_ws {

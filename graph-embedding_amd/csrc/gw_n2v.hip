@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "gw_device_common.h"
@@ -215,11 +216,53 @@ __device__ __forceinline__ int64_t draw_first_order(const gw_dev_graph& G, int64
   return (gw_u01(uy) < G.node_q[b + kk]) ? kk : (int64_t)G.node_J[b + kk];
 }
 
+// Membership pre-filter for has_edge: every row r owns 16 bits per adjacency
+// entry at bit offset 16*offsets[r]; neighbour x sets bit h(x) of its row.
+// A clear bit proves x is not a neighbour (one cache line instead of a
+// log2(deg)-probe binary search); a set bit (true hit or ~6% false positive)
+// falls through to the exact search, so results never change.
+__device__ __forceinline__ uint64_t gw_bm_bit(int64_t rowb, int64_t deg, int32_t key) {
+  const uint32_t h = (uint32_t)key * 0x9E3779B1u;
+  return 16ull * (uint64_t)rowb + (((uint64_t)h * (uint64_t)(16 * deg)) >> 32);
+}
+
+__device__ __forceinline__ bool gw_has_edge(const gw_dev_graph& G, int64_t rb, int64_t re,
+                                            int32_t key) {
+  if (G.bitmap) {
+    const uint64_t bit = gw_bm_bit(rb, re - rb, key);
+    if (!((G.bitmap[bit >> 5] >> (bit & 31)) & 1u)) return false;
+  }
+  return gw_row_find(G.nbrs, rb, re, key) >= 0;
+}
+
+__global__ void k_build_bitmap(int64_t n, const int64_t* __restrict__ off,
+                               const int32_t* __restrict__ nbrs, uint32_t* __restrict__ bm) {
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n) return;
+  const int64_t b = off[v], e = off[v + 1];
+  for (int64_t k = b; k < e; ++k) {
+    const uint64_t bit = gw_bm_bit(b, e - b, nbrs[k]);
+    atomicOr(&bm[bit >> 5], 1u << (bit & 31));
+  }
+}
+
+// One lane per walk.  The loop is flattened to ONE rejection trial per
+// iteration: a lane that accepts advances to its next step while the others
+// retry, so a wave is not held at every step by its unluckiest lane (the
+// expected maximum of 64 geometric trial counts is ~4x their mean).
+// Output: each lane stages its positions in a private LDS column and writes
+// them back 16 at a time (64 contiguous bytes per lane) instead of one
+// 4-byte store per step at a 4*L-byte lane stride.
+constexpr int kStage = 16;
+
 template <bool FIRST_ORDER, bool WEIGHTED, bool DIRECTED>
 __global__ void __launch_bounds__(kBlock)
 k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_count,
              int shuffle, int32_t* __restrict__ out, int32_t* __restrict__ lens,
              unsigned long long* __restrict__ counters) {
+  __shared__ int32_t s_stage[kBlock / 64][kStage][64];
+  const int lane = threadIdx.x & 63;
+  int32_t* stage = &s_stage[threadIdx.x >> 6][0][lane];  // slot j at stage[64*j]
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long my_steps = 0, my_trials = 0;
   if (i < walk_count) {
@@ -233,74 +276,95 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
     double w_back = 1.0;     // weight of edge cur<->prev (outlier area)
     bool back_ok = false;    // cur -> prev exists (always true undirected)
     int32_t* row = out + i * (int64_t)L;
-    row[0] = cur;
+    const bool vec_ok = (L & 3) == 0;
+    stage[0] = cur;
     int len = 1;
+    uint32_t trial = 0;
     const uint32_t c0 = (uint32_t)w, c1 = (uint32_t)((uint64_t)w >> 32);
+    int64_t b = G.offsets[cur], e = G.offsets[cur + 1];
+    double Wcur = WEIGHTED ? G.wsum[cur] : (double)(e - b);
     while (len < L) {
-      const int64_t b = G.offsets[cur], e = G.offsets[cur + 1];
       const int64_t d = e - b;
-      if (d == 0) break;
+      if (d == 0) break;  // directed sink (node2vec.py:36-37)
+      bool acc;
       int64_t slot;
       int32_t next;
       if (FIRST_ORDER || len == 1) {
         gw_u4 u = gw_philox(c0, c1, (uint32_t)len, 0u, P.k0, P.k1);
-        ++my_trials;
+        trial = 1;
         slot = b + draw_first_order<WEIGHTED>(G, b, d, u.x, u.y);
         next = G.nbrs[slot];
+        acc = true;
       } else {
-        double Wcur = WEIGHTED ? G.wsum[cur] : (double)d;
-        double out_area = (back_ok && P.extra > 0.0) ? P.extra * w_back : 0.0;
-        double A = P.M * Wcur + out_area;
-        uint32_t trial = 0;
-        for (;;) {
-          gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
-          ++trial;
-          if (out_area > 0.0 && gw_u01(u.z) * A < out_area) {  // return-edge outlier
-            slot = -1;
-            next = prev;
-            break;
-          }
-          const int64_t s = b + draw_first_order<WEIGHTED>(G, b, d, u.x, u.y);
-          const int32_t x = G.nbrs[s];
+        const gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
+        ++trial;
+        const double out_area = (back_ok && P.extra > 0.0) ? P.extra * w_back : 0.0;
+        const double A = P.M * Wcur + out_area;
+        if (out_area > 0.0 && gw_u01(u.z) * A < out_area) {  // return-edge outlier
+          slot = -1;
+          next = prev;
+          acc = true;
+        } else {
+          slot = b + draw_first_order<WEIGHTED>(G, b, d, u.x, u.y);
+          next = G.nbrs[slot];
           const double t = gw_u01(u.w) * P.M;
-          bool acc;
-          if (x == prev) {
+          if (next == prev) {
             acc = t < P.h_prev;
           } else if (t < P.lo) {
             acc = true;
           } else {
             bool adj;
             if (DIRECTED)
-              adj = gw_row_find(G.nbrs, G.offsets[x], G.offsets[x + 1], prev) >= 0;  // edge x -> prev
+              adj = gw_has_edge(G, G.offsets[next], G.offsets[next + 1], prev);  // edge x -> prev
             else
-              adj = gw_row_find(G.nbrs, pb, pe, x) >= 0;  // x in N(prev)
+              adj = gw_has_edge(G, pb, pe, next);  // x in N(prev)
             acc = t < (adj ? 1.0 : P.a_q);
           }
-          if (acc || trial >= (1u << 24)) {
-            slot = s;
-            next = x;
-            break;
+          if (trial >= (1u << 24)) acc = true;
+        }
+      }
+      if (acc) {
+        my_trials += trial;
+        trial = 0;
+        // carry state for the next step: existence/weight of edge next -> cur
+        if (DIRECTED) {
+          if (!FIRST_ORDER && P.extra > 0.0) {  // probe once per step
+            const int64_t bs = gw_row_find(G.nbrs, G.offsets[next], G.offsets[next + 1], cur);
+            back_ok = bs >= 0;
+            w_back = (back_ok && WEIGHTED) ? G.weights[bs] : 1.0;
+          }
+        } else if (slot >= 0) {
+          back_ok = true;
+          w_back = WEIGHTED ? G.weights[slot] : 1.0;
+        }  // undirected return over the same edge: w_back unchanged
+        prev = cur;
+        pb = b;
+        pe = e;
+        cur = next;
+        stage[64 * (len & (kStage - 1))] = cur;
+        if ((len & (kStage - 1)) == kStage - 1) {  // flush positions len-15 .. len
+          int32_t* dst = row + (len - (kStage - 1));
+          if (vec_ok) {
+#pragma unroll
+            for (int j = 0; j < kStage; j += 4) {
+              int4 v = make_int4(stage[64 * j], stage[64 * (j + 1)], stage[64 * (j + 2)], stage[64 * (j + 3)]);
+              *reinterpret_cast<int4*>(dst + j) = v;
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < kStage; ++j) dst[j] = stage[64 * j];
           }
         }
-        my_trials += trial;
+        ++len;
+        b = G.offsets[cur];
+        e = G.offsets[cur + 1];
+        if (WEIGHTED) Wcur = G.wsum[cur];
+        else Wcur = (double)(e - b);
       }
-      // carry state for the next step: existence/weight of edge next -> cur
-      if (DIRECTED) {
-        if (!FIRST_ORDER && P.extra > 0.0) {  // probe once per step
-          const int64_t bs = gw_row_find(G.nbrs, G.offsets[next], G.offsets[next + 1], cur);
-          back_ok = bs >= 0;
-          w_back = (back_ok && WEIGHTED) ? G.weights[bs] : 1.0;
-        }
-      } else if (slot >= 0) {
-        back_ok = true;
-        w_back = WEIGHTED ? G.weights[slot] : 1.0;
-      }  // undirected return over the same edge: w_back unchanged
-      prev = cur;
-      pb = b;
-      pe = e;
-      cur = next;
-      row[len++] = cur;
     }
+    // tail: staged positions [len & ~15, len) then -1 padding up to L
+    const int base = len & ~(kStage - 1);
+    for (int t = base; t < len; ++t) row[t] = stage[64 * (t - base)];
     for (int t = len; t < L; ++t) row[t] = -1;
     if (lens) lens[i] = len;
     my_steps = (unsigned long long)(len - 1);
@@ -338,6 +402,7 @@ void gw_dev_release(gw_graph* g) {
   dev_free(d.edge_off);
   dev_free(d.edge_J);
   dev_free(d.edge_q);
+  dev_free(d.bitmap);
   gw_topsim_ws& t = g->ts;
   dev_free(t.lvl_vertex);
   dev_free(t.lvl_parent);
@@ -453,6 +518,16 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
     GW_HIP_TRY(hipDeviceSynchronize());
     dev_free(stack);
     g->edge_alias_entries = total;
+  }
+  dev_free(d.bitmap);
+  const char* nobm = getenv("GW_DIAG_NO_BITMAP");  // diagnostic A/B knob only
+  if (mode == GW_N2V_REJECTION && !(p == 1.0 && q == 1.0) && g->nnz && !(nobm && nobm[0] == '1')) {
+    const int64_t words = (16 * g->nnz + 31) / 32 + 1;
+    if ((rc = dev_alloc(g, &d.bitmap, words))) return rc;
+    GW_HIP_TRY(hipMemset(d.bitmap, 0, sizeof(uint32_t) * words));
+    k_build_bitmap<<<grid_for(g->n), kBlock>>>(g->n, d.offsets, d.nbrs, d.bitmap);
+    GW_HIP_TRY(hipGetLastError());
+    GW_HIP_TRY(hipDeviceSynchronize());
   }
   g->p = p;
   g->q = q;
