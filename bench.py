@@ -94,14 +94,22 @@ def cpu_baseline(csr, args, sample_walk0):
                                         "(per-edge alias tables need 7.0e10 entries)"}
 
 
+def lib_digest():
+    import hashlib
+    from gwamd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def load_traffic(tag, launch_steps):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, only
+    when it was measured on this exact library build and workload."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(p) as f:
             d = json.load(f)
         e = d.get(tag)
-        if e and e.get("walk_steps_per_launch") == launch_steps:
+        if e and e.get("walk_steps_per_launch") == launch_steps and e.get("lib_sha256") == lib_digest():
             return e["hbm_bytes_per_launch"]
     except Exception:
         pass
@@ -286,7 +294,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_walk_scale<false,false,false>", "kernel_ms": k_avg_ms,
-                         "bytes_per_unit": BYTES_PER_STEP, "units_per_launch": launch_steps},
+                         "bytes_per_unit": BYTES_PER_STEP, "units_per_launch": launch_steps,
+                         "lib_sha256": lib_digest()},
             "cpu_baseline": cpu,
             "secondary": secondary,
         }

@@ -79,6 +79,19 @@ def build(force=False, verbose=False):
         _run([cxx, "-shared", "-o", OUT] + objs +
              [f"-L{ROCM}/lib", "-lamdhip64", "-fopenmp", f"-Wl,-rpath,{ROCM}/lib",
               "-Wl,--no-undefined"], verbose)
+    # C++ host mirror of the Java TopSim API + the benchmark driver binary
+    host = os.path.join(HERE, "host")
+    bindir = os.path.join(HERE, "bin")
+    os.makedirs(bindir, exist_ok=True)
+    hsrc = [os.path.join(host, "topsim_host.cpp")]
+    hhdr = [os.path.join(host, "topsim_host.hpp"), os.path.join(ROOT, "include", "graphwalk.h")]
+    for drv in ["test_u_u_topsim_singlesample"]:
+        exe = os.path.join(bindir, drv)
+        dsrc = os.path.join(host, drv + ".cpp")
+        if force or _newer(exe, hsrc + hhdr + [dsrc, OUT, __file__]):
+            _run([cxx, "-O2", "-std=c++17", "-Wall", f"-I{os.path.join(ROOT, 'include')}", "-o", exe, dsrc] + hsrc +
+                 [f"-L{os.path.dirname(OUT)}", "-lgraphwalk", "-Wl,-rpath,$ORIGIN/../gwamd",
+                  f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"], verbose)
     return OUT
 
 

@@ -43,6 +43,7 @@ def main():
     summ[tag] = {
         "kernel": walk_key,
         "walk_steps_per_launch": roof["units_per_launch"],
+        "lib_sha256": roof.get("lib_sha256"),
         "fetch_bytes_per_launch": fb,
         "write_bytes_per_launch": wb,
         "hbm_bytes_per_launch": fb + wb,
