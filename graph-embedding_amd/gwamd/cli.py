@@ -1,0 +1,109 @@
+"""node2vec walk-generation CLI, flag-compatible with node2vec/src/main.py.
+
+    python -m gwamd.cli --input graph.edgelist --delimiter ' ' --p 0.25 --q 4 \
+        --walk-length 80 --num-walks 10 --walks walks.txt [--mode replay|scale]
+
+main.py:20-73 flags are accepted with the same names, defaults and quirks
+(`--delimiter` defaults to ',' (:59); `--unweighted`/`--undirected` write to
+their own dests and never clear `weighted`/`directed` (:64, :69)).
+The embedding flags (--output, --dimensions, --window-size, --iter,
+--workers) belong to gensim's Word2Vec (main.py:92-101), which is out of
+scope: they are accepted and ignored.  Walks are written in DeepSim's
+save_list format (DeepSim/src/main.py:237-243) or as .npy.
+
+--mode replay : reference-exact (networkx graph, global random/np.random
+                seeded with --seed, per-edge alias tables on the GPU);
+--mode scale  : Philox/rejection kernel (any size; identical for any GPU count).
+"""
+import argparse
+import random
+import sys
+import time
+
+import numpy as np
+
+
+def parse_args(argv=None, p=1.0, q=1.0):
+    ap = argparse.ArgumentParser(description="Run node2vec walk generation on MI355X.")
+    ap.add_argument("--input", nargs="?", default="../graph/karate.edgelist", help="Input graph path")
+    ap.add_argument("--output", nargs="?", default=None, help="(embeddings path; gensim step not run)")
+    ap.add_argument("--walks", default="walks.txt", help="walks output (save_list format, or .npy)")
+    ap.add_argument("--dimensions", type=int, default=128)
+    ap.add_argument("--walk-length", type=int, default=80)
+    ap.add_argument("--num-walks", type=int, default=10)
+    ap.add_argument("--window-size", type=int, default=10)
+    ap.add_argument("--iter", default=10, type=int)
+    ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--p", type=float, default=p)
+    ap.add_argument("--q", type=float, default=q)
+    ap.add_argument("--delimiter", type=str, default=",")
+    ap.add_argument("--weighted", dest="weighted", action="store_true")
+    ap.add_argument("--unweighted", dest="unweighted", action="store_false")
+    ap.set_defaults(weighted=False)
+    ap.add_argument("--directed", dest="directed", action="store_true")
+    ap.add_argument("--undirected", dest="undirected", action="store_false")
+    ap.set_defaults(directed=False)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--mode", choices=["replay", "scale"], default="replay")
+    ap.add_argument("--device", type=int, default=0)
+    return ap.parse_args(argv)
+
+
+def read_graph(args):
+    """main.py:76-89 read_graph (networkx)."""
+    import networkx as nx
+    if args.weighted:
+        G = nx.read_edgelist(args.input, nodetype=int, data=(("weight", float),), create_using=nx.DiGraph(),
+                             delimiter=args.delimiter)
+    else:
+        G = nx.read_edgelist(args.input, nodetype=int, create_using=nx.DiGraph(), delimiter=args.delimiter)
+        for edge in G.edges():
+            G[edge[0]][edge[1]]["weight"] = 1
+    if not args.directed:
+        G = G.to_undirected()
+    return G
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    t0 = time.time()
+    from . import io
+    if args.mode == "replay":
+        from . import node2vec
+        random.seed(args.seed)
+        np.random.seed(args.seed)
+        nx_G = read_graph(args)
+        G = node2vec.Graph(nx_G, args.directed, args.p, args.q, device=args.device)
+        G.preprocess_transition_probs()
+        walks = G.simulate_walks(args.num_walks, args.walk_length)
+        if args.walks.endswith(".npy"):
+            W = np.full((len(walks), args.walk_length), -1, np.int64)
+            for i, w in enumerate(walks):
+                W[i, :len(w)] = w
+            np.save(args.walks, W)
+        else:
+            io.save_list(walks, args.walks)
+        nwalks = len(walks)
+    else:
+        from . import _lib as C
+        from .graph import GWGraph
+        g = GWGraph.from_edgelist(args.input, args.delimiter, "nx", args.directed, args.weighted)
+        g.to_device(args.device)
+        C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, C.N2V_REJECTION), g.handle)
+        n = g.n
+        nwalks = args.num_walks * n
+        W = np.empty((nwalks, args.walk_length), np.int32)
+        lens = np.empty(nwalks, np.int32)
+        C.check(C.lib().gw_n2v_walks_host(g.handle, args.walk_length, args.seed, 0, nwalks, 1, C.ptr(W),
+                                          C.ptr(lens), None), g.handle)
+        if args.walks.endswith(".npy"):
+            lab = g.export_csr()["labels"]
+            np.save(args.walks, np.where(W >= 0, lab[np.maximum(W, 0)], -1))
+        else:
+            io.save_walks(g, args.walks, W, lens)
+    print(f"{nwalks} walks -> {args.walks} in {time.time() - t0:.2f}s", file=sys.stderr)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -194,3 +194,26 @@ def test_replay_refuses_huge_edge_tables(gw):
     G = gw.GWGraph.rmat(18, 16, seed=1).to_device(0)
     with pytest.raises(C.CapacityError):
         C.check(C.lib().gw_n2v_prepare(G.handle, 0.25, 4.0, C.N2V_REPLAY), G.handle)
+
+
+def test_cli_replay_and_scale(gw, tmp_path):
+    """gwamd.cli (main.py flags): replay mode writes the reference walks in
+    DeepSim's save_list format; scale mode writes walks that follow edges."""
+    from gwamd import cli, io
+    g = load_golden("n2v_karate_p0.25_q4_s7.npz")
+    out = tmp_path / "walks.txt"
+    assert cli.main(["--input", os.path.join(DATA, "karate.edgelist"), "--delimiter", " ", "--p", "0.25",
+                     "--q", "4", "--seed", "7", "--walks", str(out)]) == 0
+    got = io.read_list(str(out))
+    assert [[int(x) for x in w] for w in got] == g["walks"].tolist()
+    out2 = tmp_path / "w2.npy"
+    assert cli.main(["--input", os.path.join(DATA, "karate.edgelist"), "--delimiter", " ", "--p", "0.25",
+                     "--q", "4", "--seed", "7", "--mode", "scale", "--walks", str(out2)]) == 0
+    W = np.load(str(out2))
+    assert W.shape == (340, 80)
+    adj = set()
+    for line in open(os.path.join(DATA, "karate.edgelist")):
+        a, b = map(int, line.split())
+        adj.add((a, b))
+        adj.add((b, a))
+    assert all((int(a), int(b)) in adj for a, b in zip(W[:, :-1].ravel(), W[:, 1:].ravel()))
