@@ -52,8 +52,9 @@ struct gw_topsim_ws {
   int32_t* spawn_level = nullptr; // [blocks][spawn_cap]
   int32_t* spawn_first = nullptr; // [blocks][spawn_cap+1] walker prefix
   double* spawn_mass = nullptr;   // [blocks][spawn_cap] child mass m/ceil(m)
-  double* acc_row = nullptr;      // [blocks][n] (only when n too big for LDS)
-  int32_t* touched = nullptr;     // [blocks][touch_cap]
+  double* acc_row = nullptr;      // [blocks][touch_cap] overflow hash values (hash mode)
+  int32_t* ov_keys = nullptr;     // [blocks][touch_cap] overflow hash keys (-1 empty)
+  int32_t* touched = nullptr;     // [blocks][touch_cap] claimed overflow slots
   unsigned int* src_counter = nullptr;  // work queue head
   int* error_flag = nullptr;      // capacity overflow
 };

@@ -413,6 +413,7 @@ void gw_dev_release(gw_graph* g) {
   dev_free(t.spawn_level);
   dev_free(t.spawn_first);
   dev_free(t.acc_row);
+  dev_free(t.ov_keys);
   dev_free(t.touched);
   dev_free(t.src_counter);
   dev_free(t.error_flag);

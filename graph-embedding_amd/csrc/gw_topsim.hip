@@ -39,6 +39,9 @@ constexpr int TS_BLOCK = 512;
 constexpr int TS_WAVES = TS_BLOCK / 64;
 constexpr int TOPK_MAX = 256;
 constexpr int64_t LDS_ROW_MAX_BYTES = 96 * 1024;
+constexpr int HASH_BITS = 13;                 // LDS hash: 8192 slots = 96 KB
+constexpr int HASH_SLOTS = 1 << HASH_BITS;
+constexpr int HASH_LIMIT = HASH_SLOTS * 3 / 4;  // load limit before overflowing to HBM
 
 struct TsArgs {
   gw_dev_graph G;
@@ -63,7 +66,8 @@ struct TsArgs {
   int32_t* spawn_level;
   int32_t* spawn_first;
   double* spawn_mass;
-  double* acc_row;
+  int32_t* ov_keys;
+  double* ov_vals;
   int32_t* touched;
   unsigned int* src_counter;
   int* error_flag;
@@ -126,11 +130,11 @@ __device__ __forceinline__ unsigned long long dkey(double v) {
 template <int STEP, bool LDS_ROW>
 __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
   constexpr int L = 2 * STEP;
-  extern __shared__ double s_row[];  // LDS accumulator row (LDS_ROW)
+  extern __shared__ double s_row[];  // LDS row (LDS_ROW) or hash values+keys
   __shared__ int s_wave[TS_WAVES + 1];
   __shared__ long long s_red[TS_WAVES];
   __shared__ int s_size[L + 2];
-  __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort;
+  __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount;
   __shared__ unsigned s_hist[256];
   __shared__ unsigned long long s_prefix, s_mask;
   __shared__ int32_t s_sel_id[TOPK_MAX];
@@ -149,32 +153,78 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
   int32_t* SL = A.spawn_level + blk * A.spawn_cap;
   int32_t* SF = A.spawn_first + blk * (A.spawn_cap + 1);
   double* SM = A.spawn_mass + blk * A.spawn_cap;
-  double* acc = LDS_ROW ? s_row : (A.acc_row + blk * (int64_t)n);
+  // accumulator: dense LDS row (small n) or LDS open-addressing hash with a
+  // per-workgroup HBM overflow hash (large n)
+  double* s_hval = s_row;                                   // [HASH_SLOTS]
+  int32_t* s_hkey = reinterpret_cast<int32_t*>(s_row + HASH_SLOTS);  // [HASH_SLOTS]
+  int32_t* ov_key = LDS_ROW ? nullptr : (A.ov_keys + blk * A.touch_cap);
+  double* ov_val = LDS_ROW ? nullptr : (A.ov_vals + blk * A.touch_cap);
   int32_t* touched = LDS_ROW ? nullptr : (A.touched + blk * A.touch_cap);
+  const uint32_t ov_mask = (uint32_t)(A.touch_cap - 1);
   const bool rw = (A.variant == GW_TOPSIM_SINGLE_RW);
   const bool enumerate_all = (A.variant == GW_TOPSIM_ENUMERATE);
 
   long long my_ext = 0, my_upd = 0, my_walk = 0, my_maxf = 0;
 
-  if (LDS_ROW)
+  if (LDS_ROW) {
     for (int j = tid; j < n; j += TS_BLOCK) s_row[j] = 0.0;
-  if (tid == 0) s_ntouch = 0;
+  } else {
+    for (int j = tid; j < HASH_SLOTS; j += TS_BLOCK) {
+      s_hval[j] = 0.0;
+      s_hkey[j] = -1;
+    }
+  }
+  if (tid == 0) {
+    s_ntouch = 0;
+    s_hcount = 0;
+  }
   __syncthreads();
 
-  // accumulate one pair update into the row
+  // overflow insert into the workgroup's HBM hash (slots claimed by CAS; the
+  // claimed slot is recorded for selection and cleanup)
+  auto ov_add = [&](int32_t target, double val) {
+    uint32_t h = ((uint32_t)target * 0x9E3779B1u) & ov_mask;
+    for (int64_t probe = 0; probe <= (int64_t)ov_mask; ++probe) {
+      const int32_t old = atomicCAS(&ov_key[h], -1, target);
+      if (old == -1 || old == target) {
+        if (old == -1) {
+          const int k = atomicAdd(&s_ntouch, 1);
+          if ((int64_t)k < A.touch_cap * 3 / 4) touched[k] = (int32_t)h;
+          else atomicOr(A.error_flag, 2);
+        }
+        atomicAdd(&ov_val[h], val);
+        return;
+      }
+      h = (h + 1) & ov_mask;
+    }
+    atomicOr(A.error_flag, 2);
+  };
+
+  // accumulate one pair update
   auto add = [&](int32_t target, double val) {
     if (LDS_ROW) {
-      atomicAdd(&acc[target], val);
-    } else {
-      double old = atomicAdd(&acc[target], val);
-      if (old == 0.0) {  // first touch (every update is > 0)
-        int k = atomicAdd(&s_ntouch, 1);
-        if (k < A.touch_cap)
-          touched[k] = target;
-        else
-          atomicOr(A.error_flag, 2);
-      }
+      atomicAdd(&s_row[target], val);
+      return;
     }
+    uint32_t h = ((uint32_t)target * 0x9E3779B1u) >> (32 - HASH_BITS);
+    for (int probe = 0; probe < HASH_SLOTS; ++probe) {
+      const int32_t k = s_hkey[h];
+      if (k == target) {
+        atomicAdd(&s_hval[h], val);
+        return;
+      }
+      if (k == -1) {
+        // reserve an LDS entry first; past the load limit new keys overflow
+        if (atomicAdd(&s_hcount, 1) >= HASH_LIMIT) break;
+        const int32_t old = atomicCAS(&s_hkey[h], -1, target);
+        if (old == -1 || old == target) {
+          atomicAdd(&s_hval[h], val);
+          return;
+        }
+      }
+      h = (h + 1) & (HASH_SLOTS - 1);
+    }
+    ov_add(target, val);
   };
 
   // computePathSim for the path node at depth 2i with mass `mass`
@@ -385,17 +435,56 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
     __syncthreads();
 
     // ---- output ------------------------------------------------------------
-    const int NC = LDS_ROW ? n : s_ntouch;
+    // hash mode: fold overflow entries whose key also reached the LDS table
+    // (a key can straddle the load limit) into the LDS entry
+    const int nov = LDS_ROW ? 0 : min((int64_t)s_ntouch, A.touch_cap * 3 / 4);
+    if (!LDS_ROW && nov > 0) {
+      for (int k = tid; k < nov; k += TS_BLOCK) {
+        const int32_t slot = touched[k];
+        const int32_t key = __hip_atomic_load(&ov_key[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t h = ((uint32_t)key * 0x9E3779B1u) >> (32 - HASH_BITS);
+        for (int probe = 0; probe < HASH_SLOTS; ++probe) {
+          const int32_t kk = s_hkey[h];
+          if (kk == -1) break;
+          if (kk == key) {
+            const double v = __hip_atomic_load(&ov_val[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            atomicAdd(&s_hval[h], v);
+            __hip_atomic_store(&ov_val[slot], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          h = (h + 1) & (HASH_SLOTS - 1);
+        }
+      }
+      __syncthreads();
+    }
+    const int NC = LDS_ROW ? n : HASH_SLOTS + nov;
     auto cand = [&](int idx, int32_t* id, double* val) -> bool {
-      int32_t t = LDS_ROW ? idx : touched[idx];
-      double v = acc[t];
-      *id = t;
-      *val = v;
-      return v > 0.0;
+      if (LDS_ROW) {
+        *id = idx;
+        *val = s_row[idx];
+      } else if (idx < HASH_SLOTS) {
+        *id = s_hkey[idx];
+        *val = s_hval[idx];
+      } else {
+        const int32_t slot = touched[idx - HASH_SLOTS];
+        *id = __hip_atomic_load(&ov_key[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *val = __hip_atomic_load(&ov_val[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return *val > 0.0;
     };
     if (A.out_rows) {
       double* orow = A.out_rows + r * (int64_t)n;
-      for (int t = tid; t < n; t += TS_BLOCK) orow[t] = acc[t];
+      if (LDS_ROW) {
+        for (int t = tid; t < n; t += TS_BLOCK) orow[t] = s_row[t];
+      } else {
+        for (int t = tid; t < n; t += TS_BLOCK) orow[t] = 0.0;
+        __syncthreads();
+        for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+          int32_t id;
+          double v;
+          if (cand(idx, &id, &v)) orow[id] = v;
+        }
+      }
     }
     if (A.out_ids) {
       const int K = A.topk;
@@ -540,11 +629,21 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
     if (LDS_ROW) {
       for (int t = tid; t < n; t += TS_BLOCK) s_row[t] = 0.0;
     } else {
-      const int nt = min((int64_t)s_ntouch, A.touch_cap);
-      for (int k = tid; k < nt; k += TS_BLOCK) acc[touched[k]] = 0.0;
+      for (int j = tid; j < HASH_SLOTS; j += TS_BLOCK) {
+        s_hval[j] = 0.0;
+        s_hkey[j] = -1;
+      }
+      for (int k = tid; k < nov; k += TS_BLOCK) {
+        const int32_t slot = touched[k];
+        __hip_atomic_store(&ov_key[slot], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ov_val[slot], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     __syncthreads();
-    if (tid == 0) s_ntouch = 0;
+    if (tid == 0) {
+      s_ntouch = 0;
+      s_hcount = 0;
+    }
     __syncthreads();
   }
 
@@ -581,7 +680,7 @@ void ws_free(T*& p) {
 
 template <int STEP, bool LDS>
 hipError_t launch_step(const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
-  if (LDS) {
+  {
     hipError_t e = hipFuncSetAttribute((const void*)k_topsim<STEP, LDS>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -635,6 +734,7 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   ws_free(t.spawn_first);
   ws_free(t.spawn_mass);
   ws_free(t.acc_row);
+  ws_free(t.ov_keys);
   ws_free(t.touched);
   ws_free(t.src_counter);
   ws_free(t.error_flag);
@@ -655,9 +755,17 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
     return GW_ERR_INVALID;
   }
   const bool lds_row = n * 8 <= LDS_ROW_MAX_BYTES;
-  const int64_t touch_cap = lds_row ? 1 : n;
+  // hash mode: HBM overflow table per workgroup (power of two) beyond the
+  // 6144 keys the LDS table holds; distinct targets per source are bounded by
+  // min(n, pair updates <= ~3*STEP*SAMPLE)
+  int64_t touch_cap = 1;
+  if (!lds_row) {
+    const int64_t want = std::max<int64_t>(1 << 14, std::min<int64_t>(2 * n, 4LL * step * sample));
+    touch_cap = 1;
+    while (touch_cap < want) touch_cap <<= 1;
+  }
   const int64_t per_block = (int64_t)(L + 1) * level_cap * 8 + 2 * level_cap * 8 + (level_cap + 1) * 4 +
-                            spawn_cap * 20 + 4 + (lds_row ? 0 : n * 12);
+                            spawn_cap * 20 + 4 + (lds_row ? 0 : touch_cap * 16);
   int dev_cus = 256;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, g->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
@@ -681,8 +789,10 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
       (rc = ws_alloc(g, &t.src_counter, 1)) || (rc = ws_alloc(g, &t.error_flag, 1)))
     return rc;
   if (!lds_row) {
-    if ((rc = ws_alloc(g, &t.acc_row, blocks * n))) return rc;
-    GW_HIP_TRY(hipMemset(t.acc_row, 0, sizeof(double) * blocks * n));
+    if ((rc = ws_alloc(g, &t.acc_row, blocks * touch_cap)) || (rc = ws_alloc(g, &t.ov_keys, blocks * touch_cap)))
+      return rc;
+    GW_HIP_TRY(hipMemset(t.acc_row, 0, sizeof(double) * blocks * touch_cap));
+    GW_HIP_TRY(hipMemset(t.ov_keys, 0xFF, sizeof(int32_t) * blocks * touch_cap));  // -1 = empty
   }
   t.variant = variant;
   t.sample = sample;
@@ -693,7 +803,7 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   t.spawn_cap = spawn_cap;
   t.touch_cap = touch_cap;
   t.lds_row = lds_row ? 1 : 0;
-  t.lds_bytes = lds_row ? (size_t)n * 8 : 0;
+  t.lds_bytes = lds_row ? (size_t)n * 8 : (size_t)HASH_SLOTS * 12;
   GW_HIP_TRY(hipDeviceSynchronize());
   return GW_OK;
 }
@@ -737,7 +847,8 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   A.spawn_level = t.spawn_level;
   A.spawn_first = t.spawn_first;
   A.spawn_mass = t.spawn_mass;
-  A.acc_row = t.acc_row;
+  A.ov_keys = t.ov_keys;
+  A.ov_vals = t.acc_row;
   A.touched = t.touched;
   A.src_counter = t.src_counter;
   A.error_flag = t.error_flag;
@@ -745,7 +856,7 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   GW_HIP_TRY(hipMemsetAsync(t.error_flag, 0, sizeof(int), s));
   const int blocks = (int)std::min<int64_t>(t.blocks, nsrc);
   hipError_t e = t.lds_row ? launch<true>(step, A, blocks, t.lds_bytes, s)
-                           : launch<false>(step, A, blocks, 0, s);
+                           : launch<false>(step, A, blocks, t.lds_bytes, s);
   if (e != hipSuccess) {
     g->err = std::string("k_topsim launch: ") + hipGetErrorString(e);
     return GW_ERR_DEVICE;

@@ -52,14 +52,19 @@ def test_topsim_dense_equals_oracle(gw, oracle, name, sample, step):
     assert st[0] == rst["extensions"] and st[1] == rst["pair_updates"] and st[3] == rst["walkers"]
 
 
-def test_topsim_large_n_global_row(gw, oracle):
-    """arxiv (n=38741) takes the HBM accumulator-row path."""
+@pytest.mark.parametrize("sample,stride", [(5000, 97), (40000, 1931)])
+def test_topsim_large_n_hash_accumulator(gw, oracle, sample, stride):
+    """arxiv (n=38741 > LDS row) takes the LDS-hash path; SAMPLE=40000 pushes
+    sources past the 6144-key LDS limit into the HBM overflow hash."""
     g = _graph(gw, "arxiv")
-    sources = np.arange(0, 38741, 97, dtype=np.int32)
-    rows, st = _dense_gpu(g, 0, 5000, 5, sources)
-    ref, rst = _oracle(oracle, g, 0, 5000, 5, sources)
+    sources = np.arange(0, 38741, stride, dtype=np.int32)
+    rows, st = _dense_gpu(g, 0, sample, 5, sources)
+    ref, rst = _oracle(oracle, g, 0, sample, 5, sources)
     np.testing.assert_allclose(rows, ref, rtol=1e-12, atol=1e-9)
+    assert np.array_equal(rows > 0, ref > 0)
     assert st[1] == rst["pair_updates"]
+    if sample == 40000:
+        assert (ref > 0).sum(axis=1).max() > 6144  # overflow path exercised
 
 
 @pytest.mark.parametrize("step", [1, 2])
@@ -164,3 +169,38 @@ def test_cpp_driver_matches_oracle(gw, oracle, tmp_path):
     for v in (0, 3, 500, 1379):
         exp = oracle.java_fixed_max_pq_row(rows[v], 20)
         assert got[v].decode() == f"{v}" + "".join(f"\t{i}:{oracle.java_format_fixed(x)}" for i, x in exp)
+
+
+def test_topsim_hash_overflow_rmat(gw, oracle):
+    """Hub sources of a Java-semantics R-MAT-15 graph reach > 6144 distinct
+    targets: the LDS hash overflows into the HBM hash, results unchanged."""
+    import torch
+    from gwamd import _lib as Cl
+    G = gw.GWGraph.rmat(15, 8, seed=3)
+    c = G.export_csr()
+    deg = np.diff(c["offsets"])
+    rows = np.repeat(np.arange(len(deg)), deg)
+    m = rows < c["nbrs"]
+    J = gw.GWGraph.from_edges(rows[m], c["nbrs"][m], semantics="java", vcount=len(deg))
+    jc = J.export_csr()
+    J.to_device(0)
+    top = np.argsort(-np.diff(jc["offsets"]))[:16].astype(np.int32)
+    ref, rst = oracle.topsim(jc["offsets"], jc["nbrs"], 0, 20000, 3, seed=9, sources=top, nthreads=8)
+    assert (ref > 0).sum(axis=1).max() > 6144
+    src = torch.as_tensor(top, device="cuda")
+    out = torch.empty((len(top), len(deg)), dtype=torch.float64, device="cuda")
+    st = torch.zeros(4, dtype=torch.int64, device="cuda")
+    Cl.check(Cl.lib().gw_topsim_dense(J.handle, 0, 20000, 3, 0.6, 9, Cl.ptr(src), len(top), Cl.ptr(out),
+                                      Cl.ptr(st), None), J.handle)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-12, atol=1e-9)
+    assert int(st[1]) == rst["pair_updates"]
+    # top-k path over the same overflowing rows
+    k = 100
+    ids = torch.empty((len(top), k), dtype=torch.int32, device="cuda")
+    sc = torch.empty((len(top), k), dtype=torch.float64, device="cuda")
+    Cl.check(Cl.lib().gw_topsim(J.handle, 0, 20000, 3, 0.6, 9, Cl.ptr(src), len(top), k, Cl.ptr(ids), Cl.ptr(sc),
+                                None, None), J.handle)
+    for r in range(len(top)):
+        row = ref[r]
+        order = sorted(np.nonzero(row > 0)[0].tolist(), key=lambda i: (-row[i], i))[:k]
+        np.testing.assert_allclose(sc.cpu().numpy()[r], row[order], rtol=1e-12)
