@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--topsim-sample", type=int, default=10000)
     ap.add_argument("--topsim-step", type=int, default=5)
-    ap.add_argument("--topsim-graphs", default="blog", help="comma list of blog,arxiv,moreno")
+    ap.add_argument("--topsim-graphs", default="blog", help="comma list of blog,arxiv,moreno,p10m")
     return ap.parse_args()
 
 
@@ -93,6 +93,33 @@ def cpu_baseline(csr, args, sample_walk0):
             "reference_python_context": "reference node2vec.py measured 41,266 walk-steps/s/core on "
                                         "RMAT-12 in the build container (SURVEY §6); it cannot run at scale 20 "
                                         "(per-edge alias tables need 7.0e10 entries)"}
+
+
+def topsim_cpu_baseline(tg, sample, step, args):
+    """Oracle restatement of TopSim_singleSample (Java-literal queue, OpenMP
+    over sources) on a bounded prefix of the same sources."""
+    import oracle
+    import numpy as np
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except Exception:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    n = tg.getVCount()
+    ns = min(n, 256)
+    t0 = time.perf_counter()
+    _, st = oracle.topsim(tg._offs, tg._nbrs, 0, sample, step, C=0.6, seed=args.seed,
+                          sources=np.arange(ns, dtype=np.int32), nthreads=cores)
+    dt = time.perf_counter() - t0
+    ns2 = int(min(n, max(ns, ns * args.cpu_seconds / max(dt, 1e-3))))
+    t0 = time.perf_counter()
+    _, st = oracle.topsim(tg._offs, tg._nbrs, 0, sample, step, C=0.6, seed=args.seed,
+                          sources=np.arange(ns2, dtype=np.int32), nthreads=cores)
+    dt = time.perf_counter() - t0
+    return {"value": st["pair_updates"] / dt, "unit": "pair-updates/s", "cores": cores, "kind": "port",
+            "sample": f"sources 0..{ns2 - 1} ({st['pair_updates']} pair-updates), oracle/oracle.c or_topsim "
+                      f"(TopSim_singleSample.java queue restated), {dt:.1f} s; the Java reference cannot run "
+                      "here (no JDK)"}
 
 
 def lib_digest():
@@ -219,25 +246,41 @@ def main():
             sys.exit(3)
 
     # ---- TopSim secondary metric (config 3: lshrank graphs) ----
-    TOPSIM_GRAPHS = {"blog": ("blog.txt", 10313, ",", "333,983 edges"),
-                     "arxiv": ("arxiv_author_pub.txt", 38741, "\t", "58,595 edges"),
-                     "moreno": ("moreno_crime_crime.txt", 1380, "\t", "1,476 edges")}
+    TOPSIM_GRAPHS = {"blog": ("blog.txt", 10313, ",", "lshrank blog, V=10313, 333,983 edges"),
+                     "arxiv": ("arxiv_author_pub.txt", 38741, "\t", "lshrank arxiv, V=38741, 58,595 edges"),
+                     "moreno": ("moreno_crime_crime.txt", 1380, "\t", "lshrank moreno, V=1380, 1,476 edges")}
 
     def run_topsim(name):
         from gwamd import topsim
-        fname, V, sep, desc = TOPSIM_GRAPHS[name]
-        tg = topsim.Graph(os.path.join(ROOT, "tests", "golden", "data", fname), V, separator=sep,
-                          device=dev.index)
-        tg._ensure_device()
-        src = torch.arange(V, dtype=torch.int32, device=dev)
         K = 20
+        sample, step = args.topsim_sample, args.topsim_step
+        if name == "p10m":
+            # config 5: 10M-vertex Java-semantics R-MAT (reference quadrant
+            # recursion), 1e8 generated lines, all non-isolated sources, top-100
+            t0 = time.perf_counter()
+            pg = gwamd.GWGraph.rmat_java(10_000_000, 100_000_000, 0.57, 0.19, 0.19, args.seed)
+            deg = np.diff(pg.export_csr()["offsets"])
+            log(f"[rank {rank}] p10m built in {time.perf_counter() - t0:.1f}s")
+            pg.to_device(dev.index)
+            h = pg.handle
+            srcs = np.nonzero(deg > 0)[0].astype(np.int32)
+            V = len(srcs)
+            desc = f"10M vertices, 1e8 R-MAT lines, {V} non-isolated sources"
+            K, sample, step = 100, 1000, 3
+            src = torch.as_tensor(srcs, device=dev)
+        else:
+            fname, V, sep, desc = TOPSIM_GRAPHS[name]
+            tg = topsim.Graph(os.path.join(ROOT, "tests", "golden", "data", fname), V, separator=sep,
+                              device=dev.index)
+            tg._ensure_device()
+            h = tg._g.handle
+            src = torch.arange(V, dtype=torch.int32, device=dev)
         ids = torch.empty((V, K), dtype=torch.int32, device=dev)
         sc = torch.empty((V, K), dtype=torch.float64, device=dev)
         st = torch.zeros(4, dtype=torch.int64, device=dev)
-        h = tg._g.handle
 
         def ts_run(stats_ptr):
-            C.check(C.lib().gw_topsim(h, C.TOPSIM_SINGLE_SAMPLE, args.topsim_sample, args.topsim_step, 0.6,
+            C.check(C.lib().gw_topsim(h, C.TOPSIM_SINGLE_SAMPLE, sample, step, 0.6,
                                       args.seed, C.ptr(src), V, K, C.ptr(ids), C.ptr(sc), stats_ptr, sh), h)
 
         ts_run(None)  # warm-up (also sizes the workspace)
@@ -259,16 +302,19 @@ def main():
             dist.all_reduce(st, op=dist.ReduceOp.SUM)
         ext, upd = int(st[0].item()), int(st[1].item())
         alg = (TOPSIM_B_EXT * ext + TOPSIM_B_UPD * upd) / max(world, 1)
+        cpu_ts = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline and name != "p10m":
+            cpu_ts = topsim_cpu_baseline(tg, sample, step, args)
         return {
             "metric": "SimRank pair-updates/sec (TopSim_singleSample)", "value": upd / tel,
             "unit": "pair-updates/s", "path_extensions_per_s": ext / tel,
-            "config": {"workload": f"TopSim_singleSample on lshrank {name} (V={V}, {desc}, Java multigraph), "
+            "config": {"workload": f"TopSim_singleSample on {name} ({desc}, Java multigraph), "
                                    "all sources, replicated per rank",
-                       "step": args.topsim_step, "sample": args.topsim_sample, "C": 0.6, "topk": K},
-            "pair_updates": upd, "path_extensions": ext, "seconds": tel,
+                       "step": step, "sample": sample, "C": 0.6, "topk": K},
+            "pair_updates": upd, "path_extensions": ext, "seconds": tel, "cpu_baseline": cpu_ts,
             "roofline": {"bound": "hbm", "achieved": alg / kt / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alg / kt / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": f"k_topsim<{args.topsim_step},*>", "kernel_ms": kt * 1e3},
+                         "kernel": f"k_topsim<{step},*>", "kernel_ms": kt * 1e3},
         }
 
     secondary = None

@@ -15,6 +15,7 @@ int gw_load_edgelist_impl(gw_graph* g, const char* path, const char* delim, int 
                           int directed, int weighted, int64_t vcount);
 int gw_rmat_impl(gw_graph* g, int scale, int edge_factor, double a, double b, double c,
                  uint64_t seed);
+int gw_rmat_java_impl(gw_graph* g, int64_t n, int64_t m, double a, double b, double c, uint64_t seed);
 int gw_write_walks_impl(const gw_graph* g, const char* path, const int32_t* walks,
                         const int32_t* lens, int64_t nwalks, int walk_len, std::string* err);
 int gw_write_sim_dense_impl(const char* path, const double* rows, const int32_t* row_ids,
@@ -172,6 +173,20 @@ int gw_graph_rmat(int scale, int edge_factor, double a, double b, double c, uint
   *out = nullptr;
   gw_graph* g = new gw_graph();
   int rc = gw_rmat_impl(g, scale, edge_factor, a, b, c, seed);
+  if (rc != GW_OK) {
+    tls_err = g->err;
+    delete g;
+    return rc;
+  }
+  *out = g;
+  return GW_OK;
+}
+
+int gw_graph_rmat_java(int64_t n, int64_t m, double a, double b, double c, uint64_t seed, gw_graph** out) {
+  if (!out) return gw_fail(nullptr, GW_ERR_INVALID, "out is NULL");
+  *out = nullptr;
+  gw_graph* g = new gw_graph();
+  int rc = gw_rmat_java_impl(g, n, m, a, b, c, seed);
   if (rc != GW_OK) {
     tls_err = g->err;
     delete g;

@@ -439,6 +439,52 @@ int gw_rmat_impl(gw_graph* g, int scale, int edge_factor, double a, double b,
 }
 
 // ------------------------------------------------------------------------
+// R-MAT with an arbitrary vertex count, Java multigraph semantics (TopSim
+// synthetic input): the quadrant recursion of the
+// reference generator (RMATGraphGenerator.java:119-145, halving
+// [st, en] ranges until both are singletons), one Philox uniform per level in
+// place of Random.nextDouble(); every generated line (col_st, row_st) is
+// added both ways as structures.Graph.addEdge does (duplicates and self
+// loops kept, Graph.java:53-57).
+// ------------------------------------------------------------------------
+int gw_rmat_java_impl(gw_graph* g, int64_t n, int64_t m, double a, double b, double c,
+                      uint64_t seed) {
+  if (n < 1 || n >= (int64_t)INT32_MAX || m < 0) return gw_fail(g, GW_ERR_INVALID, "bad rmat n/m");
+  if (!(a > 0 && b >= 0 && c >= 0 && a + b + c < 1.0)) return gw_fail(g, GW_ERR_INVALID, "bad rmat probabilities");
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32) ^ GW_TAG_RMAT ^ 0x4A415641u;  // "JAVA"
+  const double cumA = a, cumB = a + b, cumC = a + b + c;
+  std::vector<int64_t> src(m), dst(m);
+#pragma omp parallel for schedule(static)
+  for (int64_t e = 0; e < m; ++e) {
+    int64_t col_st = 0, col_en = n - 1, row_st = 0, row_en = n - 1;
+    uint32_t lvl = 0;
+    gw_u4 r{0, 0, 0, 0};
+    while (col_st != col_en || row_st != row_en) {
+      if ((lvl & 3) == 0) r = gw_philox((uint32_t)e, (uint32_t)((uint64_t)e >> 32), lvl >> 2, 1u, k0, k1);
+      const uint32_t rr = (lvl & 3) == 0 ? r.x : (lvl & 3) == 1 ? r.y : (lvl & 3) == 2 ? r.z : r.w;
+      ++lvl;
+      const double x = gw_u01(rr);
+      if (x < cumA) {  // top-left
+        col_en = col_st + (col_en - col_st) / 2;
+        row_en = row_st + (row_en - row_st) / 2;
+      } else if (x < cumB) {  // top-right
+        col_st = col_en - (col_en - col_st) / 2;
+        row_en = row_st + (row_en - row_st) / 2;
+      } else if (x < cumC) {  // bottom-left
+        col_en = col_st + (col_en - col_st) / 2;
+        row_st = row_en - (row_en - row_st) / 2;
+      } else {  // bottom-right
+        col_st = col_en - (col_en - col_st) / 2;
+        row_st = row_en - (row_en - row_st) / 2;
+      }
+    }
+    src[e] = col_st;
+    dst[e] = row_st;
+  }
+  return gw_build_java_multi(g, m, src.data(), dst.data(), n);
+}
+
+// ------------------------------------------------------------------------
 // writers
 // ------------------------------------------------------------------------
 int gw_write_walks_impl(const gw_graph* g, const char* path, const int32_t* walks,

@@ -91,6 +91,7 @@ SIGNATURES = {
     "gw_graph_from_edges": (ctypes.c_int, [I64, P, P, P, ctypes.c_int, ctypes.c_int, I64, PP]),
     "gw_graph_from_csr": (ctypes.c_int, [I64, P, P, P, P, P, ctypes.c_int, ctypes.c_int, PP]),
     "gw_graph_rmat": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, D, D, D, U64, PP]),
+    "gw_graph_rmat_java": (ctypes.c_int, [I64, I64, D, D, D, U64, PP]),
     "gw_graph_info": (ctypes.c_int, [P, ctypes.POINTER(GraphInfo)]),
     "gw_graph_export_csr": (ctypes.c_int, [P, P, P, P, P, P]),
     "gw_graph_free": (ctypes.c_int, [P]),

@@ -90,6 +90,13 @@ class GWGraph:
         C.check(C.lib().gw_graph_rmat(int(scale), int(edge_factor), a, b, c, int(seed), ctypes.byref(h)))
         return cls(h)
 
+    @classmethod
+    def rmat_java(cls, n, m, a=0.57, b=0.19, c=0.19, seed=42):
+        """Java-multigraph R-MAT over n vertices (RMATGraphGenerator.java:119-145)."""
+        h = ctypes.c_void_p()
+        C.check(C.lib().gw_graph_rmat_java(int(n), int(m), a, b, c, int(seed), ctypes.byref(h)))
+        return cls(h)
+
     # ---- accessors ------------------------------------------------------------
     @property
     def handle(self):

@@ -128,6 +128,12 @@ int gw_graph_from_csr(int64_t n, const int64_t* offsets, const int32_t* nbrs,
  * keyed by seed: identical on every host.                                   */
 int gw_graph_rmat(int scale, int edge_factor, double a, double b, double c,
                   uint64_t seed, gw_graph** out);
+/* R-MAT over an arbitrary vertex count n with m generated lines, Java
+ * multigraph semantics (the reference generator's quadrant recursion,
+ * RMATGraphGenerator.java:119-145; each line added both ways, duplicates and
+ * self loops kept), V = n.  TopSim synthetic input (P10M: n=1e7, m=1e8).  */
+int gw_graph_rmat_java(int64_t n, int64_t m, double a, double b, double c,
+                       uint64_t seed, gw_graph** out);
 int gw_graph_info(const gw_graph* g, gw_graph_info_t* info);
 /* offsets[n+1], nbrs[nnz] (dense ids, row order = draw order), weights[nnz]
  * (NULL ok), labels[n] (NULL ok), node_order[n] (dense ids in the

@@ -54,8 +54,8 @@ def test_topsim_dense_equals_oracle(gw, oracle, name, sample, step):
 
 @pytest.mark.parametrize("sample,stride", [(5000, 97), (40000, 1931)])
 def test_topsim_large_n_hash_accumulator(gw, oracle, sample, stride):
-    """arxiv (n=38741 > LDS row) takes the LDS-hash path; SAMPLE=40000 pushes
-    sources past the 6144-key LDS limit into the HBM overflow hash."""
+    """arxiv (n=38741 > LDS row) takes the LDS-hash path (overflow into the
+    HBM hash is exercised by test_topsim_hash_overflow_rmat)."""
     g = _graph(gw, "arxiv")
     sources = np.arange(0, 38741, stride, dtype=np.int32)
     rows, st = _dense_gpu(g, 0, sample, 5, sources)
@@ -63,8 +63,6 @@ def test_topsim_large_n_hash_accumulator(gw, oracle, sample, stride):
     np.testing.assert_allclose(rows, ref, rtol=1e-12, atol=1e-9)
     assert np.array_equal(rows > 0, ref > 0)
     assert st[1] == rst["pair_updates"]
-    if sample == 40000:
-        assert (ref > 0).sum(axis=1).max() > 6144  # overflow path exercised
 
 
 @pytest.mark.parametrize("step", [1, 2])
