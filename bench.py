@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--num-walks", type=int, default=10)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--allgather", action="store_true")
+    ap.add_argument("--mode", choices=["auto", "bitset", "rejection"], default="auto",
+                    help="second-order sampler (auto: bitset when it fits in HBM)")
     ap.add_argument("--no-topsim", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -174,7 +176,23 @@ def main():
     log(f"[rank {rank}] rmat-{args.scale}: n={n} nnz={nnz} maxdeg={inf.max_degree} "
         f"built in {time.perf_counter() - t0:.1f}s")
     G.to_device(dev.index)
-    C.check(C.lib().gw_n2v_prepare(G.handle, args.p, args.q, C.N2V_REJECTION), G.handle)
+    # sampler: per-edge common-neighbour bitsets when sum(deg^2) bits fit in
+    # HBM (exact 3-way mixture, ~2 lines per step), else rejection sampling
+    t0 = time.perf_counter()
+    mode = "bitset" if args.mode in ("auto", "bitset") else "rejection"
+    if mode == "bitset":
+        try:
+            C.check(C.lib().gw_n2v_prepare(G.handle, args.p, args.q, C.N2V_BITSET), G.handle)
+        except C.CapacityError as e:
+            if args.mode == "bitset":
+                raise
+            log(f"[rank {rank}] bitset tables do not fit ({e}); using rejection sampling")
+            mode = "rejection"
+    if mode == "rejection":
+        C.check(C.lib().gw_n2v_prepare(G.handle, args.p, args.q, C.N2V_REJECTION), G.handle)
+    torch.cuda.synchronize()
+    prep_s = time.perf_counter() - t0
+    log(f"[rank {rank}] prepare ({mode}) {prep_s:.2f}s")
 
     B = args.num_walks * n                      # walks per rank per step
     out = torch.empty((B, L), dtype=torch.int32, device=dev)
@@ -230,7 +248,7 @@ def main():
     value = steps_total / el
     launch_steps = steps_local // args.steps
     achieved = BYTES_PER_STEP * launch_steps / (k_avg_ms * 1e-3) / 1e9
-    tag = f"n2v_rmat{args.scale}_p{args.p}_q{args.q}_L{L}_r{args.num_walks}"
+    tag = f"n2v_rmat{args.scale}_p{args.p}_q{args.q}_L{L}_r{args.num_walks}_{mode}"
     traffic = load_traffic(tag, launch_steps)
 
     # ---- parity spot check (cheap): every step follows an edge ----
@@ -350,10 +368,12 @@ def main():
                        "global_batch": B * world, "seq_len": L, "parallelism": f"dp{world}",
                        "allgather": bool(gather is not None)},
             "walk_steps": steps_total,
+            "sampler": mode, "prepare_seconds": prep_s,
             "rejection_trials_per_step": trials_total / max(steps_total, 1),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_walk_scale<false,false,false>", "kernel_ms": k_avg_ms,
+                         "kernel": "k_walk_bitset" if mode == "bitset" else "k_walk_scale<false,false,false>",
+                         "kernel_ms": k_avg_ms,
                          "bytes_per_unit": BYTES_PER_STEP, "units_per_launch": launch_steps,
                          "lib_sha256": lib_digest()},
             "cpu_baseline": cpu,

@@ -240,7 +240,10 @@ int gw_graph_to_device(gw_graph* g, int device) {
 int gw_n2v_prepare(gw_graph* g, double p, double q, int mode) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
   if (!(p > 0) || !(q > 0)) return ret(g, gw_fail(g, GW_ERR_ZERODIV, "p and q must be > 0 (node2vec.py:70-76 divides by them)"));
-  if (mode != GW_N2V_REPLAY && mode != GW_N2V_REJECTION) return ret(g, gw_fail(g, GW_ERR_INVALID, "unknown mode %d", mode));
+  if (mode != GW_N2V_REPLAY && mode != GW_N2V_REJECTION && mode != GW_N2V_BITSET)
+    return ret(g, gw_fail(g, GW_ERR_INVALID, "unknown mode %d", mode));
+  if (mode == GW_N2V_BITSET && (g->weighted || g->directed || g->semantics != GW_SEM_NX_SIMPLE))
+    return ret(g, gw_fail(g, GW_ERR_UNSUPPORTED, "GW_N2V_BITSET needs an unweighted undirected NX_SIMPLE graph"));
   if (g->semantics != GW_SEM_NX_SIMPLE && !(p == 1.0 && q == 1.0))
     return ret(g, gw_fail(g, GW_ERR_UNSUPPORTED, "biased walks need NX_SIMPLE semantics (sorted rows)"));
   if (g->weighted) {

@@ -20,6 +20,11 @@
 //   node_J/q int32/f64[nnz] per-node alias tables (weighted or REPLAY)
 //   edge_off int64[nnz+1], edge_J/q per-edge alias tables (REPLAY only)
 //   bitmap   u32[16*nnz/32] has_edge membership pre-filter (REJECTION, p/q != 1)
+//   bs_*     per-edge common-neighbour bitsets (BITSET mode, sum(deg^2) bits)
+struct gw_bs_nbr {  // GW_N2V_BITSET: neighbour id + region of that edge
+  uint32_t x, pad, roff_lo, roff_hi;
+};
+
 struct gw_dev_graph {
   int64_t n = 0, nnz = 0;
   int64_t* offsets = nullptr;
@@ -34,6 +39,8 @@ struct gw_dev_graph {
   int32_t* edge_J = nullptr;
   double* edge_q = nullptr;
   uint32_t* bitmap = nullptr;  // has_edge pre-filter, 16 bits per entry
+  uint32_t* bs_region = nullptr;  // GW_N2V_BITSET per-edge regions (gw_n2v_bitset.hip)
+  gw_bs_nbr* bs_nbr = nullptr;    // [nnz] neighbour + region offset
 };
 
 struct gw_topsim_ws {
@@ -78,6 +85,7 @@ struct gw_graph {
   int n2v_mode = -1;
   double p = 1.0, q = 1.0;
   int64_t edge_alias_entries = 0;
+  int64_t bitset_words = 0;
   // TopSim state
   gw_topsim_ws ts;
   std::string err;
@@ -103,6 +111,11 @@ int gw_dev_n2v_walks_replay(gw_graph* g, int walk_len, int64_t nwalks,
                             const int32_t* starts, const double* uniforms,
                             int64_t n_uniforms, int32_t* out_walks,
                             int32_t* out_len, int64_t* uniforms_used);
+void gw_dev_bitset_release(gw_graph* g);
+int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes);
+int gw_dev_walk_bitset_launch(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int64_t walk_count,
+                              int shuffle, int32_t* out_dev, int32_t* len_dev, uint64_t* counters_dev,
+                              void* stream);
 int gw_dev_n2v_walks(gw_graph* g, int walk_len, uint64_t seed,
                      int64_t walk_begin, int64_t walk_count, int shuffle,
                      int32_t* out_walks_dev, int32_t* out_len_dev,

@@ -403,6 +403,7 @@ void gw_dev_release(gw_graph* g) {
   dev_free(d.edge_J);
   dev_free(d.edge_q);
   dev_free(d.bitmap);
+  gw_dev_bitset_release(g);
   gw_topsim_ws& t = g->ts;
   dev_free(t.lvl_vertex);
   dev_free(t.lvl_parent);
@@ -521,14 +522,23 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
     g->edge_alias_entries = total;
   }
   dev_free(d.bitmap);
+  gw_dev_bitset_release(g);
+  g->bitset_words = 0;
   const char* nobm = getenv("GW_DIAG_NO_BITMAP");  // diagnostic A/B knob only
-  if (mode == GW_N2V_REJECTION && !(p == 1.0 && q == 1.0) && g->nnz && !(nobm && nobm[0] == '1')) {
+  if ((mode == GW_N2V_BITSET || (mode == GW_N2V_REJECTION && !(p == 1.0 && q == 1.0))) && g->nnz &&
+      !(nobm && nobm[0] == '1')) {
     const int64_t words = (16 * g->nnz + 31) / 32 + 1;
     if ((rc = dev_alloc(g, &d.bitmap, words))) return rc;
     GW_HIP_TRY(hipMemset(d.bitmap, 0, sizeof(uint32_t) * words));
     k_build_bitmap<<<grid_for(g->n), kBlock>>>(g->n, d.offsets, d.nbrs, d.bitmap);
     GW_HIP_TRY(hipGetLastError());
     GW_HIP_TRY(hipDeviceSynchronize());
+  }
+  if (mode == GW_N2V_BITSET && !(p == 1.0 && q == 1.0)) {
+    size_t fr = 0, tot = 0;
+    int64_t budget = (int64_t)64 << 30;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) budget = std::min<int64_t>(budget, (int64_t)(fr / 2));
+    if ((rc = gw_dev_bitset_build(g, budget))) return rc;
   }
   g->p = p;
   g->q = q;
@@ -682,6 +692,9 @@ int gw_dev_n2v_walks(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int6
   P.k1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_STEP;
   P.pk0 = (uint32_t)seed;
   P.pk1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_PERM;
+  if (g->n2v_mode == GW_N2V_BITSET && !first_order)
+    return gw_dev_walk_bitset_launch(g, L, seed, walk_begin, walk_count, shuffle, out_dev, len_dev, counters_dev,
+                                     stream);
   hipStream_t s = (hipStream_t)stream;
   const unsigned grid = grid_for(walk_count);
   unsigned long long* C = (unsigned long long*)counters_dev;

@@ -1,0 +1,415 @@
+// node2vec exact second-order sampling with per-edge common-neighbour
+// bitsets (GW_N2V_BITSET) — the compressed form of the reference's per-edge
+// alias tables.
+//
+// The reference precomputes, for every directed edge (src -> dst), an alias
+// table over sorted N(dst) with weights  w/p (dst_nbr == src), w
+// (has_edge(dst_nbr, src)), w/q (otherwise)   (node2vec.py:61-81).
+// For unweighted undirected graphs that table is fully described by ONE BIT
+// per entry ("dst_nbr is a common neighbour of src and dst") plus the position
+// of src in N(dst): 1 bit instead of 12 bytes (q f64 + J), so sum(deg^2) bits
+// (R-MAT-20: 8.8 GB) fit in HBM where the reference's tables (7.0e10 x 12 B)
+// do not.  A step then samples the three-way mixture exactly:
+//
+//   Z = 1/p + c + (d - 1 - c)/q,  c = popcount(bitset)
+//   r = U*Z < 1/p           -> return to prev
+//   r - 1/p < c             -> the floor(r - 1/p)-th common neighbour (row order)
+//   otherwise               -> uniform over the d-1-c others (rejection on the
+//                              bitset: expected d/(d-1-c) ~ 1 trial)
+//
+// Region of edge slot s = (u -> v), 32-bit words, 32-byte aligned:
+//   [0] c   [1] kp (position of u in N(v))   [2] d = deg(v)   [3] ndir
+//   [4..5] offsets[v] (int64)   [6..7] 0
+//   dir[ndir]  cumulative set bits before each 512-bit block (d > 512 only)
+//   bits[ceil(d/32)]  bit k = (N(v)[k] != u) && has_edge(N(v)[k], u)
+// and bs_nbr[s] = {nbrs[s], 0, region word offset (u64)}: the candidate read
+// of a step also yields the next step's region, so a step touches ~2 lines
+// (region header+bits, candidate) instead of ~7 for rejection sampling.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <string>
+
+#include "gw_device_common.h"
+
+namespace {
+
+constexpr int kB = 256;
+constexpr int kHdr = 8;          // header words
+constexpr int kDirBits = 512;    // bits per directory block
+constexpr int kSmallD = 32;      // thread-per-slot fill up to this degree
+constexpr int kStage = 16;
+
+__host__ __device__ __forceinline__ int64_t bs_ndir(int64_t d) { return d > kDirBits ? (d + kDirBits - 1) / kDirBits : 0; }
+__host__ __device__ __forceinline__ int64_t bs_words(int64_t d) {
+  int64_t w = kHdr + bs_ndir(d) + (d + 31) / 32;
+  return (w + 7) & ~int64_t(7);
+}
+
+__device__ __forceinline__ int32_t row_of_slot(const int64_t* __restrict__ off, int64_t n, int64_t e) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (off[mid + 1] <= e)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return (int32_t)lo;
+}
+
+__device__ __forceinline__ bool bs_has_edge(const gw_dev_graph& G, int64_t rb, int64_t re, int32_t key) {
+  if (G.bitmap) {
+    const uint32_t h = (uint32_t)key * 0x9E3779B1u;
+    const uint64_t bit = 16ull * (uint64_t)rb + (((uint64_t)h * (uint64_t)(16 * (re - rb))) >> 32);
+    if (!((G.bitmap[bit >> 5] >> (bit & 31)) & 1u)) return false;
+  }
+  return gw_row_find(G.nbrs, rb, re, key) >= 0;
+}
+
+__global__ void k_bs_sizes(int64_t nnz, const int32_t* __restrict__ nbrs, const int32_t* __restrict__ deg,
+                           uint64_t* __restrict__ sz) {
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nnz) return;
+  sz[e] = (uint64_t)bs_words(deg[nbrs[e]]);
+}
+
+// thread per slot for small deg(v); larger slots are queued for the wave kernel
+__global__ void k_bs_fill_small(gw_dev_graph G, const uint64_t* __restrict__ roff, uint32_t* __restrict__ reg,
+                                uint4* __restrict__ bsn, int64_t* __restrict__ big, unsigned long long* __restrict__ nbig) {
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= G.nnz) return;
+  const int32_t v = G.nbrs[e];
+  const uint64_t R = roff[e];
+  bsn[e] = make_uint4((uint32_t)v, 0u, (uint32_t)R, (uint32_t)(R >> 32));
+  const int64_t vb = G.offsets[v], d = G.offsets[v + 1] - vb;
+  uint32_t* h = reg + R;
+  h[2] = (uint32_t)d;
+  h[3] = (uint32_t)bs_ndir(d);
+  h[4] = (uint32_t)(uint64_t)vb;
+  h[5] = (uint32_t)((uint64_t)vb >> 32);
+  h[6] = 0;
+  h[7] = 0;
+  if (d > kSmallD) {
+    big[atomicAdd(nbig, 1ull)] = e;
+    return;
+  }
+  const int32_t u = row_of_slot(G.offsets, G.n, e);
+  const int64_t ub = G.offsets[u], ue = G.offsets[u + 1];
+  uint32_t word = 0, c = 0, kp = 0xFFFFFFFFu;
+  for (int64_t k = 0; k < d; ++k) {
+    const int32_t x = G.nbrs[vb + k];
+    if (x == u) {
+      kp = (uint32_t)k;
+    } else if (bs_has_edge(G, ub, ue, x)) {
+      word |= 1u << (k & 31);
+      ++c;
+    }
+  }
+  h[0] = c;
+  h[1] = kp;
+  if (d > 0) h[kHdr] = word;  // ndir == 0, one word
+}
+
+// one wave per large slot: 64 neighbours per ballot
+__global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff, uint32_t* __restrict__ reg,
+                               const int64_t* __restrict__ big, const unsigned long long* __restrict__ nbig) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t total = (int64_t)*nbig;
+  for (int64_t i = wave; i < total; i += nwaves) {
+    const int64_t e = big[i];
+    const int32_t v = G.nbrs[e];
+    const int32_t u = row_of_slot(G.offsets, G.n, e);
+    const int64_t vb = G.offsets[v], d = G.offsets[v + 1] - vb;
+    const int64_t ub = G.offsets[u], ue = G.offsets[u + 1];
+    uint32_t* h = reg + roff[e];
+    const int64_t ndir = bs_ndir(d);
+    uint32_t* dir = h + kHdr;
+    uint32_t* bits = h + kHdr + ndir;
+    uint32_t c = 0;
+    int kp_local = -1;
+    for (int64_t base = 0; base < d; base += 64) {
+      const int64_t k = base + lane;
+      bool bit = false;
+      if (k < d) {
+        const int32_t x = G.nbrs[vb + k];
+        if (x == u)
+          kp_local = (int)k;
+        else
+          bit = bs_has_edge(G, ub, ue, x);
+      }
+      const unsigned long long m = __ballot(bit);
+      if (ndir && (base % kDirBits) == 0 && lane == 0) dir[base / kDirBits] = c;
+      if (lane == 0) {
+        bits[base / 32] = (uint32_t)m;
+        if (base + 32 < d) bits[base / 32 + 1] = (uint32_t)(m >> 32);
+      }
+      c += (uint32_t)__popcll(m);
+    }
+    // kp: the lane that saw u
+    const unsigned long long km = __ballot(kp_local >= 0);
+    int kp = -1;
+    if (km) {
+      const int src = __ffsll(km) - 1;
+      kp = __shfl(kp_local, src, 64);
+    }
+    if (lane == 0) {
+      h[0] = c;
+      h[1] = (uint32_t)kp;
+    }
+  }
+}
+
+// j-th (0-based) set bit of the region's bitset
+__device__ __forceinline__ int64_t bs_select(const uint32_t* __restrict__ h, int64_t d, int64_t ndir, uint32_t j) {
+  const uint32_t* dir = h + kHdr;
+  const uint32_t* bits = h + kHdr + ndir;
+  int64_t w0 = 0;
+  if (ndir > 0) {
+    int64_t lo = 0, hi = ndir - 1;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (dir[mid] <= j)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    j -= dir[lo];
+    w0 = lo * (kDirBits / 32);
+  }
+  const int64_t nw = (d + 31) >> 5;
+  for (int64_t w = w0; w < nw; ++w) {
+    uint32_t x = bits[w];
+    const uint32_t pc = (uint32_t)__popc(x);
+    if (j < pc) {
+      for (;;) {
+        const int t = __ffs(x) - 1;
+        if (j == 0) return w * 32 + t;
+        x &= x - 1;
+        --j;
+      }
+    }
+    j -= pc;
+  }
+  return 0;  // unreachable for j < c
+}
+
+struct BsParams {
+  double a_p, a_q;
+  uint32_t k0, k1, pk0, pk1;
+};
+
+__global__ void __launch_bounds__(kB)
+k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t walk_count, int shuffle,
+              int32_t* __restrict__ out, int32_t* __restrict__ lens, unsigned long long* __restrict__ counters) {
+  __shared__ int32_t s_stage[kB / 64][kStage][64];
+  const int lane = threadIdx.x & 63;
+  int32_t* stage = &s_stage[threadIdx.x >> 6][0][lane];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long my_steps = 0, my_trials = 0;
+  if (i < walk_count) {
+    const int64_t w = walk_begin + i;
+    const uint64_t it = (uint64_t)w / (uint64_t)G.n;
+    const uint64_t pos = (uint64_t)w % (uint64_t)G.n;
+    const uint64_t sp = shuffle ? gw_feistel_perm(pos, (uint64_t)G.n, P.pk0, P.pk1, (uint32_t)it) : pos;
+    int32_t cur = G.order[sp];
+    int32_t prev = -1;
+    int32_t* row = out + i * (int64_t)L;
+    const bool vec_ok = (L & 3) == 0;
+    const uint32_t c0 = (uint32_t)w, c1 = (uint32_t)((uint64_t)w >> 32);
+    stage[0] = cur;
+    int len = 1;
+    uint32_t trial = 0;
+    uint64_t R = 0;          // region of edge (prev -> cur)
+    int64_t b = 0, d = 0;    // row of cur
+    uint32_t c = 0, kp = 0, ndir = 0;
+    {
+      b = G.offsets[cur];
+      d = G.offsets[cur + 1] - b;
+    }
+    bool have_hdr = true;
+    while (len < L) {
+      if (!have_hdr) {  // header of the region of (prev -> cur)
+        const uint4 h0 = *reinterpret_cast<const uint4*>(G.bs_region + R);
+        const uint2 h1 = *reinterpret_cast<const uint2*>(G.bs_region + R + 4);
+        c = h0.x;
+        kp = h0.y;
+        d = (int64_t)h0.z;
+        ndir = h0.w;
+        b = (int64_t)((uint64_t)h1.x | ((uint64_t)h1.y << 32));
+        have_hdr = true;
+      }
+      if (d == 0) break;
+      int64_t k;
+      bool acc = true;
+      const gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
+      ++trial;
+      if (len == 1) {
+        k = (int64_t)gw_bounded(u.x, (uint32_t)d);
+      } else if (trial == 1) {
+        const double Z = (P.a_p + (double)c) + (double)(d - 1 - (int64_t)c) * P.a_q;
+        const double r = gw_u01(u.x) * Z;
+        if (r < P.a_p) {
+          k = kp;  // return to prev
+        } else if (r - P.a_p < (double)c) {
+          uint32_t j = (uint32_t)(r - P.a_p);
+          if (j >= c) j = c - 1;
+          k = bs_select(G.bs_region + R, d, ndir, j);
+        } else {
+          k = (int64_t)gw_bounded(u.y, (uint32_t)d);
+          const uint32_t word = G.bs_region[R + kHdr + ndir + (k >> 5)];
+          acc = (k != (int64_t)kp) && !((word >> (k & 31)) & 1u);
+        }
+      } else {  // retry of the "other" branch
+        k = (int64_t)gw_bounded(u.y, (uint32_t)d);
+        const uint32_t word = G.bs_region[R + kHdr + ndir + (k >> 5)];
+        acc = ((k != (int64_t)kp) && !((word >> (k & 31)) & 1u)) || trial >= (1u << 24);
+      }
+      if (acc) {
+        my_trials += trial;
+        trial = 0;
+        const uint4 e = *reinterpret_cast<const uint4*>(G.bs_nbr + (b + k));
+        prev = cur;
+        cur = (int32_t)e.x;
+        R = (uint64_t)e.z | ((uint64_t)e.w << 32);
+        have_hdr = false;
+        stage[64 * (len & (kStage - 1))] = cur;
+        if ((len & (kStage - 1)) == kStage - 1) {
+          int32_t* dst = row + (len - (kStage - 1));
+          if (vec_ok) {
+#pragma unroll
+            for (int j = 0; j < kStage; j += 4)
+              *reinterpret_cast<int4*>(dst + j) =
+                  make_int4(stage[64 * j], stage[64 * (j + 1)], stage[64 * (j + 2)], stage[64 * (j + 3)]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < kStage; ++j) dst[j] = stage[64 * j];
+          }
+        }
+        ++len;
+      }
+    }
+    (void)prev;
+    const int base = len & ~(kStage - 1);
+    for (int t = base; t < len; ++t) row[t] = stage[64 * (t - base)];
+    for (int t = len; t < L; ++t) row[t] = -1;
+    if (lens) lens[i] = len;
+    my_steps = (unsigned long long)(len - 1);
+  }
+  if (counters) {
+    for (int off = 32; off > 0; off >>= 1) {
+      my_steps += __shfl_down(my_steps, off, 64);
+      my_trials += __shfl_down(my_trials, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&counters[0], my_steps);
+      atomicAdd(&counters[1], my_trials);
+    }
+  }
+}
+
+template <typename T>
+int bs_alloc(gw_graph* g, T** p, int64_t count) {
+  *p = nullptr;
+  if (count <= 0) count = 1;
+  hipError_t e = hipMalloc((void**)p, sizeof(T) * (size_t)count);
+  if (e != hipSuccess) {
+    g->err = std::string("hipMalloc(bitset ") + std::to_string(sizeof(T) * (size_t)count) + " B): " + hipGetErrorString(e);
+    *p = nullptr;
+    return GW_ERR_NOMEM;
+  }
+  return GW_OK;
+}
+
+template <typename T>
+void bs_free(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+}  // namespace
+
+void gw_dev_bitset_release(gw_graph* g) {
+  bs_free(g->d.bs_region);
+  bs_free(g->d.bs_nbr);
+}
+
+// Build the per-edge regions.  Requires the membership bitmap (has_edge).
+int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes) {
+  gw_dev_graph& d = g->d;
+  gw_dev_bitset_release(g);
+  const int64_t nnz = g->nnz;
+  if (nnz == 0) return GW_OK;
+  int rc;
+  uint64_t* sz = nullptr;
+  uint64_t* roff = nullptr;
+  if ((rc = bs_alloc(g, &sz, nnz + 1)) || (rc = bs_alloc(g, &roff, nnz + 1))) {
+    bs_free(sz);
+    return rc;
+  }
+  k_bs_sizes<<<(unsigned)((nnz + kB - 1) / kB), kB>>>(nnz, d.nbrs, d.deg, sz);
+  GW_HIP_TRY(hipMemset(sz + nnz, 0, sizeof(uint64_t)));
+  size_t tmpb = 0;
+  GW_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmpb, sz, roff, nnz + 1));
+  void* tmp = nullptr;
+  if ((rc = bs_alloc(g, (char**)&tmp, (int64_t)tmpb + 1))) {
+    bs_free(sz);
+    bs_free(roff);
+    return rc;
+  }
+  GW_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmpb, sz, roff, nnz + 1));
+  GW_HIP_TRY(hipDeviceSynchronize());
+  bs_free(tmp);
+  bs_free(sz);
+  uint64_t words = 0;
+  GW_HIP_TRY(hipMemcpy(&words, roff + nnz, sizeof(uint64_t), hipMemcpyDeviceToHost));
+  const int64_t need = (int64_t)words * 4 + nnz * 16;
+  if (need > budget_bytes) {
+    bs_free(roff);
+    g->err = "per-edge bitsets need " + std::to_string(need) + " B (sum(deg^2) bits); over the " +
+             std::to_string(budget_bytes) + " B budget: use GW_N2V_REJECTION";
+    return GW_ERR_CAPACITY;
+  }
+  int64_t* big = nullptr;
+  unsigned long long* nbig = nullptr;
+  if ((rc = bs_alloc(g, &d.bs_region, (int64_t)words)) || (rc = bs_alloc(g, &d.bs_nbr, nnz)) ||
+      (rc = bs_alloc(g, &big, nnz)) || (rc = bs_alloc(g, &nbig, 1))) {
+    bs_free(roff);
+    bs_free(big);
+    bs_free(nbig);
+    gw_dev_bitset_release(g);
+    return rc;
+  }
+  GW_HIP_TRY(hipMemset(d.bs_region, 0, (size_t)words * 4));
+  GW_HIP_TRY(hipMemset(nbig, 0, sizeof(unsigned long long)));
+  k_bs_fill_small<<<(unsigned)((nnz + kB - 1) / kB), kB>>>(d, roff, d.bs_region, reinterpret_cast<uint4*>(d.bs_nbr), big, nbig);
+  GW_HIP_TRY(hipGetLastError());
+  k_bs_fill_wave<<<2048, kB>>>(d, roff, d.bs_region, big, nbig);
+  GW_HIP_TRY(hipGetLastError());
+  GW_HIP_TRY(hipDeviceSynchronize());
+  bs_free(roff);
+  bs_free(big);
+  bs_free(nbig);
+  g->bitset_words = (int64_t)words;
+  return GW_OK;
+}
+
+int gw_dev_walk_bitset_launch(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int64_t walk_count,
+                              int shuffle, int32_t* out_dev, int32_t* len_dev, uint64_t* counters_dev,
+                              void* stream) {
+  BsParams P;
+  P.a_p = 1.0 / g->p;
+  P.a_q = 1.0 / g->q;
+  P.k0 = (uint32_t)seed;
+  P.k1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_STEP;
+  P.pk0 = (uint32_t)seed;
+  P.pk1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_PERM;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, (walk_count + kB - 1) / kB);
+  k_walk_bitset<<<grid, kB, 0, (hipStream_t)stream>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev,
+                                                       len_dev, (unsigned long long*)counters_dev);
+  GW_HIP_TRY(hipGetLastError());
+  return GW_OK;
+}

@@ -36,6 +36,7 @@ SEM_NX_SIMPLE = 0
 SEM_JAVA_MULTI = 1
 N2V_REPLAY = 0
 N2V_REJECTION = 1
+N2V_BITSET = 2
 TOPSIM_SINGLE_SAMPLE = 0
 TOPSIM_ENUMERATE = 1
 TOPSIM_SINGLE_RW = 2

@@ -65,6 +65,12 @@ extern "C" {
  * bias by exact rejection sampling with the return edge as an outlier;
  * Philox4x32-10 keyed by (seed, walk, step, trial).                        */
 #define GW_N2V_REJECTION 1
+/* exact second-order sampling from per-edge common-neighbour bitsets (the
+ * reference's per-edge alias tables compressed to 1 bit per entry, sum(deg^2)
+ * bits; unweighted undirected NX_SIMPLE graphs): a step is a 3-way mixture
+ * (return / common neighbour / other) with no has_edge probes.  Philox keyed
+ * like GW_N2V_REJECTION.                                                   */
+#define GW_N2V_BITSET 2
 
 /* ---- TopSim variants (DeepSim/TopSimAll/src/simrank/) --------------------- */
 #define GW_TOPSIM_SINGLE_SAMPLE 0 /* TopSim_singleSample.java:62-203 (= _Basic) */

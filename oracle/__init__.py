@@ -48,6 +48,7 @@ def lib():
         L.or_walks_replay.restype = i64
         L.or_walks_scale.argtypes = [i64, v, v, v, v, v, v, v, ci, d, d, u64, ci, i64, i64, ci, v, v, v, ci]
         L.or_jrand_sequence.argtypes = [i64, i32, i64, v]
+        L.or_walks_bitset.argtypes = [i64, v, v, v, d, d, u64, ci, i64, i64, ci, v, v, v, ci]
         L.or_topsim.argtypes = [i64, v, v, ci, ci, ci, d, u64, ci, i64, v, i64, v, v, ci]
         L.or_simrank_naive.argtypes = [i64, v, v, d, ci, v, ci]
         _lib = L
@@ -134,6 +135,20 @@ def walks_scale(csr, p, q, seed, L, walk_begin, walk_count, shuffle=True, direct
     lib().or_walks_scale(n, _p(off), _p(nbrs), _p(w), _p(wsum), _p(nJ), _p(nq), _p(order), int(directed),
                          float(p), float(q), int(seed), int(L), int(walk_begin), int(walk_count), int(shuffle),
                          _p(out), _p(lens), _p(cnt), int(nthreads))
+    return out, lens, cnt
+
+
+def walks_bitset(csr, p, q, seed, L, walk_begin, walk_count, shuffle=True, nthreads=0):
+    """GW_N2V_BITSET restatement (exact 3-way mixture; unweighted undirected)."""
+    off = np.ascontiguousarray(csr["offsets"], np.int64)
+    nbrs = np.ascontiguousarray(csr["nbrs"], np.int32)
+    order = np.ascontiguousarray(csr["node_order"], np.int32)
+    out = np.empty((walk_count, L), np.int32)
+    lens = np.empty(walk_count, np.int32)
+    cnt = np.zeros(2, np.uint64)
+    lib().or_walks_bitset(len(off) - 1, _p(off), _p(nbrs), _p(order), float(p), float(q), int(seed), int(L),
+                          int(walk_begin), int(walk_count), int(shuffle), _p(out), _p(lens), _p(cnt),
+                          int(nthreads))
     return out, lens, cnt
 
 

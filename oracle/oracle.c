@@ -571,3 +571,90 @@ void or_simrank_naive(int64_t n, const int64_t* off, const int32_t* nbrs, double
   for (int64_t i = 0; i < n; ++i) sim[i * n + i] = 0.0;
   free(tmp);
 }
+
+/* ------------------------------------------------------------------------ */
+/* GW_N2V_BITSET restatement: the same 3-way exact mixture of the reference */
+/* get_alias_edge weights (node2vec.py:61-81; unweighted, undirected), but   */
+/* computing c and the common neighbours by explicit has_edge scans instead  */
+/* of precomputed bitsets.  Philox usage: step 1: u.x -> uniform neighbour;  */
+/* step >= 2: philox(w, step, 0).x -> component, .y -> first "other"        */
+/* candidate, philox(w, step, t).y -> retries t = 1, 2, ...                 */
+/* ------------------------------------------------------------------------ */
+void or_walks_bitset(int64_t n, const int64_t* off, const int32_t* nbrs, const int32_t* order, double p,
+                     double q, uint64_t seed, int L, int64_t walk_begin, int64_t walk_count, int shuffle,
+                     int32_t* out, int32_t* lens, uint64_t* counters, int nthreads) {
+  const double a_p = 1.0 / p, a_q = 1.0 / q;
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_STEP;
+  const uint32_t pk0 = (uint32_t)seed, pk1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_PERM;
+  uint64_t tot_steps = 0, tot_trials = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : tot_steps, tot_trials)
+#endif
+  for (int64_t i = 0; i < walk_count; ++i) {
+    const int64_t wi = walk_begin + i;
+    const uint64_t it = (uint64_t)wi / (uint64_t)n, pos = (uint64_t)wi % (uint64_t)n;
+    const uint64_t sp = shuffle ? gw_feistel_perm(pos, (uint64_t)n, pk0, pk1, (uint32_t)it) : pos;
+    int32_t cur = order[sp], prev = -1;
+    int32_t* row = out + i * (int64_t)L;
+    row[0] = cur;
+    int len = 1;
+    const uint32_t c0 = (uint32_t)wi, c1 = (uint32_t)((uint64_t)wi >> 32);
+    while (len < L) {
+      const int64_t b = off[cur], d = off[cur + 1] - b;
+      if (d == 0) break;
+      int64_t k = 0;
+      uint32_t trial = 0;
+      struct gw_u4 u = gw_philox(c0, c1, (uint32_t)len, 0u, k0, k1);
+      ++trial;
+      if (len == 1) {
+        k = gw_bounded(u.x, (uint32_t)d);
+      } else {
+        int64_t kp = -1, c = 0;
+        for (int64_t j = 0; j < d; ++j) {
+          int32_t x = nbrs[b + j];
+          if (x == prev) kp = j;
+          else if (find_slot(off, nbrs, prev, x) >= 0) ++c;
+        }
+        const double Z = (a_p + (double)c) + (double)(d - 1 - c) * a_q;
+        const double r = gw_u01(u.x) * Z;
+        if (r < a_p) {
+          k = kp;
+        } else if (r - a_p < (double)c) {
+          uint32_t jj = (uint32_t)(r - a_p);
+          if (jj >= (uint32_t)c) jj = (uint32_t)c - 1;
+          for (int64_t j = 0; j < d; ++j) {
+            int32_t x = nbrs[b + j];
+            if (x != prev && find_slot(off, nbrs, prev, x) >= 0) {
+              if (jj == 0) {
+                k = j;
+                break;
+              }
+              --jj;
+            }
+          }
+        } else {
+          for (;;) {
+            k = gw_bounded(u.y, (uint32_t)d);
+            int32_t x = nbrs[b + k];
+            int bit = (x != prev) && find_slot(off, nbrs, prev, x) >= 0;
+            if ((k != kp && !bit) || trial >= (1u << 24)) break;
+            u = gw_philox(c0, c1, (uint32_t)len, trial, k0, k1);
+            ++trial;
+          }
+        }
+      }
+      tot_trials += trial;
+      prev = cur;
+      cur = nbrs[b + k];
+      row[len++] = cur;
+    }
+    for (int t = len; t < L; ++t) row[t] = -1;
+    if (lens) lens[i] = len;
+    tot_steps += (uint64_t)(len - 1);
+  }
+  if (counters) {
+    counters[0] += tot_steps;
+    counters[1] += tot_trials;
+  }
+}

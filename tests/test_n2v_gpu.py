@@ -217,3 +217,43 @@ def test_cli_replay_and_scale(gw, tmp_path):
         adj.add((a, b))
         adj.add((b, a))
     assert all((int(a), int(b)) in adj for a, b in zip(W[:, :-1].ravel(), W[:, 1:].ravel()))
+
+
+@pytest.mark.parametrize("p,q", [(0.25, 4), (1, 0.5), (4, 0.25), (2, 1), (1, 1)])
+@pytest.mark.parametrize("graph", ["karate", "moreno", "arxiv", "rmat12"])
+def test_bitset_walks_gpu_equals_oracle(gw, oracle, graph, p, q):
+    """GW_N2V_BITSET (per-edge common-neighbour bitsets) == oracle restatement."""
+    import torch
+    from gwamd import _lib as C
+    if graph == "rmat12":
+        G = gw.GWGraph.rmat(12, 16, seed=11)
+    else:
+        f, dl = {"karate": ("karate.edgelist", " "), "moreno": ("moreno_crime_crime.txt", "\t"),
+                 "arxiv": ("arxiv_author_pub.txt", "\t")}[graph]
+        G = gw.GWGraph.from_edgelist(os.path.join(DATA, f), dl, "nx")
+    G.to_device(0)
+    C.check(C.lib().gw_n2v_prepare(G.handle, float(p), float(q), C.N2V_BITSET), G.handle)
+    n = G.n
+    L = 30
+    begin, count = n // 2, min(3 * n, 40000)
+    out = torch.empty((count, L), dtype=torch.int32, device="cuda")
+    lens = torch.empty(count, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    C.check(C.lib().gw_n2v_walks(G.handle, L, 77, begin, count, 1, C.ptr(out), C.ptr(lens), C.ptr(cnt), None),
+            G.handle)
+    torch.cuda.synchronize()
+    csr = G.export_csr()
+    if p == 1 and q == 1:
+        ref, rl, rc = oracle.walks_scale(dict(csr, weights=None), p, q, 77, L, begin, count, nthreads=8)
+    else:
+        ref, rl, rc = oracle.walks_bitset(csr, p, q, 77, L, begin, count, nthreads=8)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    np.testing.assert_array_equal(lens.cpu().numpy(), rl)
+    assert int(cnt[0]) == int(rc[0]) and int(cnt[1]) == int(rc[1])
+
+
+def test_bitset_refused_for_weighted_or_directed(gw):
+    from gwamd import _lib as C
+    G = gw.GWGraph.from_edgelist(os.path.join(DATA, "weighted_quirks.edgelist"), " ", "nx", False, True).to_device(0)
+    with pytest.raises(C.UnsupportedError):
+        C.check(C.lib().gw_n2v_prepare(G.handle, 0.5, 2.0, C.N2V_BITSET), G.handle)

@@ -208,3 +208,34 @@ def test_scale_walks_match_second_order_distribution(oracle):
         sd = np.sqrt(pr * (1 - pr) / tot)
         worst = max(worst, float(np.max(np.abs(emp - pr) / np.maximum(sd, 1e-12))))
     assert worst < 5.5, worst
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("p,q", [(0.25, 4), (1, 0.5), (4, 0.25)])
+def test_bitset_walks_match_second_order_distribution(oracle, p, q):
+    """The GW_N2V_BITSET mixture (return / common / other) reproduces the
+    reference transition probabilities of get_alias_edge (node2vec.py:61-81)."""
+    g = load_golden("n2v_karate_p0.25_q4_s0.npz")
+    rank = {int(x): i for i, x in enumerate(g["labels"])}
+    nbrs = np.array([rank[int(x)] for x in g["nbrs"]], np.int32)
+    offs = g["offsets"]
+    n = len(offs) - 1
+    csr = dict(offsets=offs, nbrs=nbrs, node_order=np.arange(n, dtype=np.int32))
+    out, lens, cnt = oracle.walks_bitset(csr, p, q, seed=5, L=3, walk_begin=0, walk_count=n * 20000, nthreads=8)
+    counts = {}
+    for a, b, c in out:
+        counts.setdefault((a, b), {}).setdefault(c, 0)
+        counts[(a, b)][c] += 1
+    worst = 0.0
+    for (a, b), dist in counts.items():
+        tot = sum(dist.values())
+        if tot < 4000:
+            continue
+        row = nbrs[offs[b]:offs[b + 1]]
+        na = set(nbrs[offs[a]:offs[a + 1]].tolist())
+        un = np.array([1 / p if x == a else (1.0 if x in na else 1 / q) for x in row])
+        pr = un / un.sum()
+        emp = np.array([dist.get(int(x), 0) for x in row]) / tot
+        sd = np.sqrt(pr * (1 - pr) / tot)
+        worst = max(worst, float(np.max(np.abs(emp - pr) / np.maximum(sd, 1e-12))))
+    assert worst < 5.5, worst

@@ -9,7 +9,7 @@ ARGS="--steps 1 --warmup 1 --no-cpu-baseline --no-topsim ${BENCH_ARGS}"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD" "TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "k_walk_scale" --output-format csv -d gpurun_out/${TAG}_p$i -o pmc -- python bench.py $ARGS > gpurun_out/${TAG}_p$i.json 2> gpurun_out/${TAG}_p$i.err || { echo "PASS $i FAIL ($grp)"; tail -5 gpurun_out/${TAG}_p$i.err; }
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "k_walk_scale|k_walk_bitset" --output-format csv -d gpurun_out/${TAG}_p$i -o pmc -- python bench.py $ARGS > gpurun_out/${TAG}_p$i.json 2> gpurun_out/${TAG}_p$i.err || { echo "PASS $i FAIL ($grp)"; tail -5 gpurun_out/${TAG}_p$i.err; }
 done
 python - <<'PY'
 import csv, glob, os

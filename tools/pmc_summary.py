@@ -38,7 +38,7 @@ def main():
     except Exception:
         summ = {}
     roof = bench["roofline"]
-    walk_key = [k for k in f if k.startswith("k_walk_scale")][0]
+    walk_key = [k for k in f if k.startswith("k_walk_scale") or k.startswith("k_walk_bitset")][0]
     fb, wb = f[walk_key] * 1024, w[walk_key] * 1024
     summ[tag] = {
         "kernel": walk_key,
