@@ -21,8 +21,10 @@
 //   edge_off int64[nnz+1], edge_J/q per-edge alias tables (REPLAY only)
 //   bitmap   u32[16*nnz/32] has_edge membership pre-filter (REJECTION, p/q != 1)
 //   bs_*     per-edge common-neighbour bitsets (BITSET mode, sum(deg^2) bits)
-struct gw_bs_nbr {  // GW_N2V_BITSET: neighbour id + region of that edge
-  uint32_t x, pad, roff_lo, roff_hi;
+struct gw_bs_nbr {  // GW_N2V_BITSET: one 32 B entry per adjacency slot (u -> x)
+  uint32_t x, kp, c, d;          // neighbour, position of u in N(x), #common, deg(x)
+  uint32_t off_lo, off_hi;       // offsets[x]
+  uint32_t roff_lo, roff_hi;     // word offset of the edge's bitset region
 };
 
 struct gw_dev_graph {

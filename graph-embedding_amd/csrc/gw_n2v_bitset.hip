@@ -17,14 +17,15 @@
 //   otherwise               -> uniform over the d-1-c others (rejection on the
 //                              bitset: expected d/(d-1-c) ~ 1 trial)
 //
-// Region of edge slot s = (u -> v), 32-bit words, 32-byte aligned:
-//   [0] c   [1] kp (position of u in N(v))   [2] d = deg(v)   [3] ndir
-//   [4..5] offsets[v] (int64)   [6..7] 0
-//   dir[ndir]  cumulative set bits before each 512-bit block (d > 512 only)
-//   bits[ceil(d/32)]  bit k = (N(v)[k] != u) && has_edge(N(v)[k], u)
-// and bs_nbr[s] = {nbrs[s], 0, region word offset (u64)}: the candidate read
-// of a step also yields the next step's region, so a step touches ~2 lines
-// (region header+bits, candidate) instead of ~7 for rejection sampling.
+// Per edge slot s = (u -> v):
+//   bs_nbr[s] (32 B, one line): v, kp (position of u in N(v)), c, d = deg(v),
+//            offsets[v] (int64), region word offset (u64)
+//   region   dir[ndir]  cumulative set bits before each 512-bit block
+//                       (d > 512 only), then
+//            bits[ceil(d/32)]  bit k = (N(v)[k] != u) && has_edge(N(v)[k], u)
+// The entry chosen by a step carries everything the next step needs, so a
+// step touches ~2 lines (the chosen entry, one bitset word) instead of ~7 for
+// rejection sampling.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -36,15 +37,14 @@
 namespace {
 
 constexpr int kB = 256;
-constexpr int kHdr = 8;          // header words
+constexpr int kHdr = 0;          // no in-region header (metadata lives in bs_nbr)
 constexpr int kDirBits = 512;    // bits per directory block
 constexpr int kSmallD = 32;      // thread-per-slot fill up to this degree
 constexpr int kStage = 16;
 
 __host__ __device__ __forceinline__ int64_t bs_ndir(int64_t d) { return d > kDirBits ? (d + kDirBits - 1) / kDirBits : 0; }
 __host__ __device__ __forceinline__ int64_t bs_words(int64_t d) {
-  int64_t w = kHdr + bs_ndir(d) + (d + 31) / 32;
-  return (w + 7) & ~int64_t(7);
+  return kHdr + bs_ndir(d) + (d + 31) / 32;
 }
 
 __device__ __forceinline__ int32_t row_of_slot(const int64_t* __restrict__ off, int64_t n, int64_t e) {
@@ -77,44 +77,48 @@ __global__ void k_bs_sizes(int64_t nnz, const int32_t* __restrict__ nbrs, const 
 
 // thread per slot for small deg(v); larger slots are queued for the wave kernel
 __global__ void k_bs_fill_small(gw_dev_graph G, const uint64_t* __restrict__ roff, uint32_t* __restrict__ reg,
-                                uint4* __restrict__ bsn, int64_t* __restrict__ big, unsigned long long* __restrict__ nbig) {
+                                gw_bs_nbr* __restrict__ bsn, int64_t* __restrict__ big,
+                                unsigned long long* __restrict__ nbig) {
   int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= G.nnz) return;
   const int32_t v = G.nbrs[e];
   const uint64_t R = roff[e];
-  bsn[e] = make_uint4((uint32_t)v, 0u, (uint32_t)R, (uint32_t)(R >> 32));
   const int64_t vb = G.offsets[v], d = G.offsets[v + 1] - vb;
-  uint32_t* h = reg + R;
-  h[2] = (uint32_t)d;
-  h[3] = (uint32_t)bs_ndir(d);
-  h[4] = (uint32_t)(uint64_t)vb;
-  h[5] = (uint32_t)((uint64_t)vb >> 32);
-  h[6] = 0;
-  h[7] = 0;
+  gw_bs_nbr en;
+  en.x = (uint32_t)v;
+  en.kp = 0xFFFFFFFFu;
+  en.c = 0;
+  en.d = (uint32_t)d;
+  en.off_lo = (uint32_t)(uint64_t)vb;
+  en.off_hi = (uint32_t)((uint64_t)vb >> 32);
+  en.roff_lo = (uint32_t)R;
+  en.roff_hi = (uint32_t)(R >> 32);
   if (d > kSmallD) {
+    bsn[e] = en;  // c, kp filled by k_bs_fill_wave
     big[atomicAdd(nbig, 1ull)] = e;
     return;
   }
   const int32_t u = row_of_slot(G.offsets, G.n, e);
   const int64_t ub = G.offsets[u], ue = G.offsets[u + 1];
-  uint32_t word = 0, c = 0, kp = 0xFFFFFFFFu;
+  uint32_t word = 0, c = 0;
   for (int64_t k = 0; k < d; ++k) {
     const int32_t x = G.nbrs[vb + k];
     if (x == u) {
-      kp = (uint32_t)k;
+      en.kp = (uint32_t)k;
     } else if (bs_has_edge(G, ub, ue, x)) {
       word |= 1u << (k & 31);
       ++c;
     }
   }
-  h[0] = c;
-  h[1] = kp;
-  if (d > 0) h[kHdr] = word;  // ndir == 0, one word
+  en.c = c;
+  bsn[e] = en;
+  if (d > 0) reg[R] = word;  // ndir == 0, one word
 }
 
 // one wave per large slot: 64 neighbours per ballot
 __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff, uint32_t* __restrict__ reg,
-                               const int64_t* __restrict__ big, const unsigned long long* __restrict__ nbig) {
+                               gw_bs_nbr* __restrict__ bsn, const int64_t* __restrict__ big,
+                               const unsigned long long* __restrict__ nbig) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -157,8 +161,8 @@ __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff
       kp = __shfl(kp_local, src, 64);
     }
     if (lane == 0) {
-      h[0] = c;
-      h[1] = (uint32_t)kp;
+      bsn[e].c = c;
+      bsn[e].kp = (uint32_t)kp;
     }
   }
 }
@@ -224,24 +228,9 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
     int len = 1;
     uint32_t trial = 0;
     uint64_t R = 0;          // region of edge (prev -> cur)
-    int64_t b = 0, d = 0;    // row of cur
+    int64_t b = G.offsets[cur], d = G.offsets[cur + 1] - b;  // row of cur
     uint32_t c = 0, kp = 0, ndir = 0;
-    {
-      b = G.offsets[cur];
-      d = G.offsets[cur + 1] - b;
-    }
-    bool have_hdr = true;
     while (len < L) {
-      if (!have_hdr) {  // header of the region of (prev -> cur)
-        const uint4 h0 = *reinterpret_cast<const uint4*>(G.bs_region + R);
-        const uint2 h1 = *reinterpret_cast<const uint2*>(G.bs_region + R + 4);
-        c = h0.x;
-        kp = h0.y;
-        d = (int64_t)h0.z;
-        ndir = h0.w;
-        b = (int64_t)((uint64_t)h1.x | ((uint64_t)h1.y << 32));
-        have_hdr = true;
-      }
       if (d == 0) break;
       int64_t k;
       bool acc = true;
@@ -271,11 +260,16 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
       if (acc) {
         my_trials += trial;
         trial = 0;
-        const uint4 e = *reinterpret_cast<const uint4*>(G.bs_nbr + (b + k));
+        const uint4* ep = reinterpret_cast<const uint4*>(G.bs_nbr + (b + k));
+        const uint4 e0 = ep[0], e1 = ep[1];  // one 32 B entry: next step's metadata
         prev = cur;
-        cur = (int32_t)e.x;
-        R = (uint64_t)e.z | ((uint64_t)e.w << 32);
-        have_hdr = false;
+        cur = (int32_t)e0.x;
+        kp = e0.y;
+        c = e0.z;
+        d = (int64_t)e0.w;
+        b = (int64_t)((uint64_t)e1.x | ((uint64_t)e1.y << 32));
+        R = (uint64_t)e1.z | ((uint64_t)e1.w << 32);
+        ndir = (uint32_t)bs_ndir(d);
         stage[64 * (len & (kStage - 1))] = cur;
         if ((len & (kStage - 1)) == kStage - 1) {
           int32_t* dst = row + (len - (kStage - 1));
@@ -366,7 +360,7 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes) {
   bs_free(sz);
   uint64_t words = 0;
   GW_HIP_TRY(hipMemcpy(&words, roff + nnz, sizeof(uint64_t), hipMemcpyDeviceToHost));
-  const int64_t need = (int64_t)words * 4 + nnz * 16;
+  const int64_t need = (int64_t)words * 4 + nnz * (int64_t)sizeof(gw_bs_nbr);
   if (need > budget_bytes) {
     bs_free(roff);
     g->err = "per-edge bitsets need " + std::to_string(need) + " B (sum(deg^2) bits); over the " +
@@ -385,9 +379,9 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes) {
   }
   GW_HIP_TRY(hipMemset(d.bs_region, 0, (size_t)words * 4));
   GW_HIP_TRY(hipMemset(nbig, 0, sizeof(unsigned long long)));
-  k_bs_fill_small<<<(unsigned)((nnz + kB - 1) / kB), kB>>>(d, roff, d.bs_region, reinterpret_cast<uint4*>(d.bs_nbr), big, nbig);
+  k_bs_fill_small<<<(unsigned)((nnz + kB - 1) / kB), kB>>>(d, roff, d.bs_region, d.bs_nbr, big, nbig);
   GW_HIP_TRY(hipGetLastError());
-  k_bs_fill_wave<<<2048, kB>>>(d, roff, d.bs_region, big, nbig);
+  k_bs_fill_wave<<<2048, kB>>>(d, roff, d.bs_region, d.bs_nbr, big, nbig);
   GW_HIP_TRY(hipGetLastError());
   GW_HIP_TRY(hipDeviceSynchronize());
   bs_free(roff);
