@@ -233,7 +233,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
     while (len < L) {
       if (d == 0) break;
       int64_t k;
-      bool need_bit = false;
+      bool acc = true;
       const gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
       ++trial;
       if (len == 1) {
@@ -249,22 +249,19 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
           k = bs_select(G.bs_region + R, d, ndir, j);
         } else {
           k = (int64_t)gw_bounded(u.y, (uint32_t)d);
-          need_bit = true;
+          const uint32_t word = G.bs_region[R + kHdr + ndir + (k >> 5)];
+          acc = (k != (int64_t)kp) && !((word >> (k & 31)) & 1u);
         }
       } else {  // retry of the "other" branch
         k = (int64_t)gw_bounded(u.y, (uint32_t)d);
-        need_bit = true;
+        const uint32_t word = G.bs_region[R + kHdr + ndir + (k >> 5)];
+        acc = ((k != (int64_t)kp) && !((word >> (k & 31)) & 1u)) || trial >= (1u << 24);
       }
-      // issue the bitset word and the candidate's entry together: the entry
-      // is consumed only if the candidate is accepted (~94% in "other")
-      uint32_t word = 0;
-      if (need_bit) word = G.bs_region[R + kHdr + ndir + (k >> 5)];
-      const uint4* ep = reinterpret_cast<const uint4*>(G.bs_nbr + (b + k));
-      const uint4 e0 = ep[0], e1 = ep[1];  // one 32 B entry: next step's metadata
-      const bool acc = !need_bit || ((k != (int64_t)kp) && !((word >> (k & 31)) & 1u)) || trial >= (1u << 24);
       if (acc) {
         my_trials += trial;
         trial = 0;
+        const uint4* ep = reinterpret_cast<const uint4*>(G.bs_nbr + (b + k));
+        const uint4 e0 = ep[0], e1 = ep[1];  // one 32 B entry: next step's metadata
         prev = cur;
         cur = (int32_t)e0.x;
         kp = e0.y;
