@@ -39,6 +39,7 @@ BYTES_PER_STEP = 36       # row bounds 16 + alias q/J 12 + nbr 4 + 
 TOPSIM_B_EXT = 52         # per path-extension
 TOPSIM_B_UPD = 24         # per pair-update
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
+RANDOM_LINE_PEAK = 4.8e10 # measured: random 4 B gathers, one per 128 B line, 8 GiB buffer (tools/calib)
 
 
 def parse():
@@ -140,7 +141,7 @@ def load_traffic(tag, launch_steps):
             d = json.load(f)
         e = d.get(tag)
         if e and e.get("walk_steps_per_launch") == launch_steps and e.get("lib_sha256") == lib_digest():
-            return e["hbm_bytes_per_launch"]
+            return e
     except Exception:
         pass
     return None
@@ -254,7 +255,16 @@ def main():
     launch_steps = steps_local // args.steps
     achieved = BYTES_PER_STEP * launch_steps / (k_avg_ms * 1e-3) / 1e9
     tag = f"n2v_rmat{args.scale}_p{args.p}_q{args.q}_L{L}_r{args.num_walks}_{mode}"
-    traffic = load_traffic(tag, launch_steps)
+    prof = load_traffic(tag, launch_steps)
+    traffic = prof["hbm_bytes_per_launch"] if prof else None
+    # random-line roofline: the kernel's 64 B fabric read requests per second
+    # against the calibrated random-gather rate (tools/calib: 4.8e10 lines/s)
+    line_rate = None
+    if prof and prof.get("fabric_read_requests_per_launch"):
+        lr = prof["fabric_read_requests_per_launch"] / (k_avg_ms * 1e-3)
+        line_rate = {"achieved_lines_per_s": lr, "calibrated_peak_lines_per_s": RANDOM_LINE_PEAK,
+                     "frac": lr / RANDOM_LINE_PEAK,
+                     "lines_per_step": prof["fabric_read_requests_per_launch"] / max(launch_steps, 1)}
 
     # ---- parity spot check (cheap): every step follows an edge ----
     if rank == 0:
@@ -380,7 +390,7 @@ def main():
                          "kernel": "k_walk_bitset" if mode == "bitset" else "k_walk_scale<false,false,false>",
                          "kernel_ms": k_avg_ms,
                          "bytes_per_unit": BYTES_PER_STEP, "units_per_launch": launch_steps,
-                         "lib_sha256": lib_digest()},
+                         "lib_sha256": lib_digest(), "random_line_roofline": line_rate},
             "cpu_baseline": cpu,
             "secondary": secondary,
         }

@@ -30,6 +30,9 @@ def main():
     tag, fcsv, wcsv, bjson = sys.argv[1:5]
     f = per_kernel(fcsv, "FETCH_SIZE")
     w = per_kernel(wcsv, "WRITE_SIZE")
+    lines = per_kernel(sys.argv[5], "TCC_EA0_RDREQ_sum") if len(sys.argv) > 5 else {}
+    hits = per_kernel(sys.argv[5], "TCC_HIT_sum") if len(sys.argv) > 5 else {}
+    miss = per_kernel(sys.argv[5], "TCC_MISS_sum") if len(sys.argv) > 5 else {}
     bench = json.load(open(bjson))
     out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                             "pmc_summary.json")
@@ -50,6 +53,9 @@ def main():
         "algorithmic_bytes_per_launch": roof["bytes_per_unit"] * roof["units_per_launch"],
         "fetch_bytes_per_step": fb / roof["units_per_launch"],
         "write_bytes_per_step": wb / roof["units_per_launch"],
+        "fabric_read_requests_per_launch": lines.get(walk_key),
+        "l2_hit_rate": (hits[walk_key] / (hits[walk_key] + miss[walk_key])) if walk_key in hits else None,
+        "kernel_ms": roof.get("kernel_ms"),
         "note": "FETCH_SIZE/WRITE_SIZE (KiB) x 1024, mean over dispatches, separate --pmc passes; "
                 "FETCH_SIZE not doubled (random gathers, not 16 B/lane streaming)",
     }
