@@ -326,6 +326,14 @@ int gw_topsim_dense(gw_graph* g, int variant, int sample, int step, double C, ui
                               out_rows_dev, stats_dev, stream));
 }
 
+int gw_simrank_naive(gw_graph* g, double C, int iters, double* sim_dev, void* stream) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  if (g->device < 0) return ret(g, gw_fail(g, GW_ERR_STATE, "graph is not on a device"));
+  if (g->directed) return ret(g, gw_fail(g, GW_ERR_UNSUPPORTED, "naive SimRank needs an undirected graph"));
+  if (iters < 0 || (g->n > 0 && !sim_dev)) return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
+  return ret(g, gw_dev_simrank_naive(g, C, iters, sim_dev, stream));
+}
+
 int gw_write_walks_text(const gw_graph* g, const char* path, const int32_t* walks,
                         const int32_t* lens, int64_t nwalks, int walk_len) {
   if (!g || !path || (nwalks > 0 && !walks) || walk_len < 1)

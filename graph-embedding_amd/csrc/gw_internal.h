@@ -90,6 +90,13 @@ struct gw_graph {
   int64_t bitset_words = 0;
   // TopSim state
   gw_topsim_ws ts;
+  // naive SimRank workspace (gw_simrank.hip)
+  double* sr_work = nullptr;   // m*m doubles (U = A S), m = non-isolated vertices
+  double* sr_x = nullptr;      // m*m compact S when m < n (else the output is used)
+  uint32_t* sr_ent = nullptr;  // [nnz + pad] compact neighbour | head-of-row flag
+  int64_t* sr_off = nullptr;   // [m+1] compact offsets
+  int32_t* sr_rows = nullptr;  // [m] compact id -> vertex
+  int64_t sr_n = 0, sr_m = 0;
   std::string err;
 };
 
@@ -114,6 +121,8 @@ int gw_dev_n2v_walks_replay(gw_graph* g, int walk_len, int64_t nwalks,
                             int64_t n_uniforms, int32_t* out_walks,
                             int32_t* out_len, int64_t* uniforms_used);
 void gw_dev_bitset_release(gw_graph* g);
+void gw_dev_simrank_release(gw_graph* g);
+int gw_dev_simrank_naive(gw_graph* g, double C, int iters, double* sim_dev, void* stream);
 int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes);
 int gw_dev_walk_bitset_launch(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int64_t walk_count,
                               int shuffle, int32_t* out_dev, int32_t* len_dev, uint64_t* counters_dev,

@@ -404,6 +404,7 @@ void gw_dev_release(gw_graph* g) {
   dev_free(d.edge_q);
   dev_free(d.bitmap);
   gw_dev_bitset_release(g);
+  gw_dev_simrank_release(g);
   gw_topsim_ws& t = g->ts;
   dev_free(t.lvl_vertex);
   dev_free(t.lvl_parent);

@@ -5,7 +5,8 @@ Host-side mirror of the reference interfaces over the libgraphwalk C ABI
 
 * `gwamd.node2vec`  — node2vec/src/node2vec.py (Graph, alias_setup, alias_draw)
 * `gwamd.topsim`    — DeepSim/TopSimAll structures.Graph, TopSim_singleSample,
-                      TopSim_Enumerate, SingleRandomWalk, Print.printByOrder,
+                      TopSim_Enumerate, SingleRandomWalk, SimRank (naive),
+                      Print.printByOrder/printByOrderAll,
                       Eval.precision
 * `gwamd.graph`     — owning handle over a gw_graph (edgelist / networkx /
                       R-MAT constructors)

@@ -10,6 +10,8 @@
 
 `TopSim_Enumerate` (TopSim_Enumerate.java, walks source 0 only by default)
 and `SingleRandomWalk` (SingleRandomWalk.java) use the same kernel.
+`SimRank` (SimRank.java, the naive all-pairs ground truth) runs on the GPU
+as two sparse row-gather passes per round; `printByOrderAll` is its writer.
 
 Randomness: the reference draws from an unseeded static java.util.Random
 (Graph.java:17); here every random child is a Philox draw keyed by
@@ -154,6 +156,60 @@ class TopSim_Enumerate(_TopSimBase):
 class SingleRandomWalk(_TopSimBase):
     """SingleRandomWalk.java:28-92 (scores divided by SAMPLE)."""
     VARIANT = C.TOPSIM_SINGLE_RW
+
+
+class SimRank:
+    """simrank.SimRank (SimRank.java:15-82): naive SimRank, STEP = 3 rounds
+    (the reference's private field; `step` overrides it), C from
+    MyConfiguration.C.  getResult() is the dense V x V matrix with a zero
+    diagonal (postProcess, :62-65).  Needs V*V doubles on the device."""
+    STEP = 3
+
+    def __init__(self, g, C_=C_DEFAULT, step=None):
+        self.g = g
+        self.COUNT = g.getVCount()
+        self.C = float(C_)
+        self.STEP = SimRank.STEP if step is None else int(step)
+        self._sim = None
+
+    def compute(self):
+        import torch
+        g = self.g
+        g._ensure_device()
+        dev = torch.device("cuda", g.device)
+        sim = torch.empty((self.COUNT, self.COUNT), dtype=torch.float64, device=dev)
+        h = g._g.handle
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        C.check(C.lib().gw_simrank_naive(h, self.C, self.STEP, C.ptr(sim), stream), h)
+        self._sim = sim.cpu().numpy()
+
+    def sim(self, v, w):
+        """SimRank.java:67-77: one round for the pair (v, w) from the current
+        matrix (the identity before compute(); host arithmetic, O(deg^2))."""
+        if v == w:
+            return 1.0
+        g = self.g
+        dv, dw = g.degree(v), g.degree(w)
+        if dv == 0 or dw == 0:
+            return 0.0
+        S = self._sim if self._sim is not None else np.eye(self.COUNT)
+        result = 0.0
+        for vn in g.neighbors(v):
+            for wn in g.neighbors(w):
+                result += float(S[vn, wn])
+        return self.C * result / (dv * dw)
+
+    def getResult(self):
+        if self._sim is None:
+            raise RuntimeError("call compute() first")
+        return self._sim
+
+
+def printByOrderAll(sim, outPath, topk=1000, testTopK=10, separator=SEPARATOR):
+    """Print.printByOrderAll (Print.java:55-84): printByOrder with `%.7f`."""
+    if isinstance(sim, SimRank):
+        sim = sim.getResult()
+    printByOrder(sim, outPath, topk, testTopK, separator=separator, decimals=7)
 
 
 def printByOrder(sim, outPath, topk=TOPK, testTopK=None, separator=SEPARATOR, decimals=6):

@@ -98,6 +98,24 @@ void TopSimBase::topK(int k, std::vector<int32_t>& ids, std::vector<double>& sco
                            (int64_t)src.size(), k, ids.data(), scores.data(), nullptr, st),
             g_.handle());
 }
+
+void SimRank::compute() {
+  const int64_t V = g_.getVCount();
+  sim_.assign((size_t)(V * V), 0.0);
+  gw::check(gw_simrank_naive_host(g_.handle(), conf::MyConfiguration::C, STEP, sim_.data()), g_.handle());
+}
+
+double SimRank::sim(int v, int w) const {
+  if (v == w) return 1;
+  const int dv = g_.degree(v), dw = g_.degree(w);
+  if (dv == 0 || dw == 0) return 0;
+  const int64_t V = g_.getVCount();
+  double result = 0;
+  for (int vn : g_.neighbors(v))
+    for (int wn : g_.neighbors(w))
+      result += sim_.empty() ? (vn == wn ? 1.0 : 0.0) : sim_[(size_t)vn * V + wn];
+  return conf::MyConfiguration::C * result / (dv * dw);
+}
 }  // namespace simrank
 
 namespace utils {
@@ -117,6 +135,11 @@ void Print::printByOrder(const simrank::TopSimBase& sim, const std::string& outP
 void Print::printByOrder(const std::vector<double>& sim, int64_t V, const std::string& outPath, int topk, int) {
   gw::check(gw_write_sim_text_dense(outPath.c_str(), sim.data(), nullptr, (int64_t)(sim.size() / V), V, topk,
                                     conf::MyConfiguration::SEPARATOR.c_str(), 6));
+}
+
+void Print::printByOrderAll(const std::vector<double>& sim, int64_t V, const std::string& outPath, int topk, int) {
+  gw::check(gw_write_sim_text_dense(outPath.c_str(), sim.data(), nullptr, (int64_t)(sim.size() / V), V, topk,
+                                    conf::MyConfiguration::SEPARATOR.c_str(), 7));
 }
 
 static std::vector<std::string> split(const std::string& s, const std::string& sep) {

@@ -120,6 +120,21 @@ class SingleRandomWalk : public TopSimBase {
   SingleRandomWalk(structures::Graph& g, int sample, int step, uint64_t seed = 0)
       : TopSimBase(g, sample, step, GW_TOPSIM_SINGLE_RW, seed) {}
 };
+
+// simrank.SimRank (SimRank.java:15-82): naive all-pairs SimRank on the GPU.
+class SimRank {
+ public:
+  explicit SimRank(structures::Graph& g, int step = 3) : g_(g), STEP(step) {}  // STEP = 3 (:16)
+  void compute();                                                            // :36-57 + postProcess
+  double sim(int v, int w) const;                                            // :67-77, one round
+  const std::vector<double>& getResult() const { return sim_; }              // :79-81, V*V row-major
+  int getVCount() const { return g_.getVCount(); }
+
+ private:
+  structures::Graph& g_;
+  int STEP;
+  std::vector<double> sim_;
+};
 }  // namespace simrank
 
 namespace utils {
@@ -128,6 +143,9 @@ struct Print {
   static void printByOrder(const simrank::TopSimBase& sim, const std::string& outPath, int topk, int testTopK);
   static void printByOrder(const std::vector<double>& sim, int64_t V, const std::string& outPath, int topk,
                            int testTopK);
+  // Print.printByOrderAll (Print.java:55-84): same with "%.7f"
+  static void printByOrderAll(const std::vector<double>& sim, int64_t V, const std::string& outPath, int topk,
+                              int testTopK);
 };
 struct Eval {
   // Eval.precision(path1, path2, prePath, K) (Eval.java:81-131)

@@ -226,6 +226,20 @@ int gw_topsim_host(gw_graph* g, int variant, int sample, int step, double C,
                    int topk, int32_t* out_ids, double* out_scores,
                    double* out_rows, int64_t* stats);
 
+/* ---- naive SimRank (TopSim ground truth) ------------------------------------ */
+/* Replaces new SimRank(g).compute() + getResult() (SimRank.java:21-57, 79):
+ * S := I; `iters` rounds (the reference's STEP = 3) of
+ *   S'[v][w] = C * sum_{a in N(v), b in N(w)} S[a][b] / (deg(v)*deg(w)),
+ * S'[v][v] = 1, 0 for isolated v or w; then diag := 0 (postProcess, :62-65).
+ * sim_dev: n*n doubles row-major on the graph's device (symmetric).  Needs an
+ * undirected graph (Java multigraph: duplicate entries count).  The n*n fp64
+ * workspace is kept in the handle.  fp64 result equals the reference up to
+ * summation order (tested at rtol 1e-12).                                   */
+int gw_simrank_naive(gw_graph* g, double C, int iters, double* sim_dev,
+                     void* stream);
+/* Host-buffer form (synchronous): sim[n*n].                                 */
+int gw_simrank_naive_host(gw_graph* g, double C, int iters, double* sim);
+
 /* ---- output writers (host) ------------------------------------------------ */
 /* DeepSim save_list format (DeepSim/src/main.py:237-243): one walk per line,
  * every label followed by '\t', then '\n'.  walks: dense ids (-1 padded).   */

@@ -246,7 +246,7 @@ def java_format_fixed(v, decimals=6):
     """Java 8 String.format("%.Nf", v): shortest repr digits, HALF_UP."""
     d = decimal.Decimal(repr(float(v)))
     q = decimal.Decimal(1).scaleb(-decimals)
-    return str(d.quantize(q, rounding=decimal.ROUND_HALF_UP))
+    return format(d.quantize(q, rounding=decimal.ROUND_HALF_UP), "f")
 
 
 def java_fixed_max_pq_row(row, topk):

@@ -155,6 +155,20 @@ def test_sim_writer_java_exact(gw, oracle, tmp_path):
         assert ids_lines[v].decode() == f"{v}" + "".join(f",{i}" for i, _ in exp)
 
 
+def test_sim_writer_print_by_order_all(gw, oracle, tmp_path):
+    """Print.printByOrderAll (Print.java:55-84): %.7f, topk 1000 > row length."""
+    from gwamd import topsim
+    rng = np.random.RandomState(1)
+    rows = np.round(rng.rand(12, 30) * 64) / 64 * 1e-6
+    rows[2, 3] = 5e-08
+    out = tmp_path / "a.txt"
+    topsim.printByOrderAll(rows, str(out), 1000, 10)
+    lines = open(str(out) + ".sim.txt", "rb").read().split(b"\r\n")
+    for v in range(12):
+        exp = oracle.java_fixed_max_pq_row(rows[v], 1000)
+        assert lines[v].decode() == f"{v}" + "".join(f",{i}:{oracle.java_format_fixed(x, 7)}" for i, x in exp)
+
+
 def test_precision_metric(tmp_path):
     """Eval.precision (Eval.java:81-131)."""
     from gwamd import topsim
@@ -177,3 +191,9 @@ def test_compute_calls_fail_loudly_without_gpu(gw):
     with pytest.raises(Exception):
         from gwamd.node2vec import alias_setup
         alias_setup([0.5, 0.5])
+    # naive SimRank refuses a graph that is not on a device (no host compute)
+    import numpy as np
+    from gwamd import _lib as C
+    out = np.zeros(34 * 34)
+    with pytest.raises(C.StateError):
+        C.check(C.lib().gw_simrank_naive_host(G.handle, 0.6, 3, C.ptr(out)), G.handle)

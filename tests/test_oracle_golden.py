@@ -173,6 +173,9 @@ def test_java_format_and_pq(oracle):
     assert f(0.1234565) == "0.123457"   # HALF_UP on the shortest repr digits
     assert f(1.0000005) == "1.000001"   # C printf would give 1.000000
     assert f(153.5) == "153.500000"
+    assert f(0.0, 7) == "0.0000000"     # printByOrderAll's %.7f (Print.java:77)
+    assert f(5e-08, 7) == "0.0000001"
+    assert f(1.5e-08, 7) == "0.0000000"
     # FixedMaxPQ tie order: k=2, offers 1.0,1.0,2.0 -> root (id 0) evicted
     got = oracle.java_fixed_max_pq_row([1.0, 1.0, 2.0], 2)
     assert [i for i, _ in got] == [2, 1]
