@@ -21,11 +21,23 @@
 //   edge_off int64[nnz+1], edge_J/q per-edge alias tables (REPLAY only)
 //   bitmap   u32[16*nnz/32] has_edge membership pre-filter (REJECTION, p/q != 1)
 //   bs_*     per-edge common-neighbour bitsets (BITSET mode, sum(deg^2) bits)
-struct gw_bs_nbr {  // GW_N2V_BITSET: one 32 B entry per adjacency slot (u -> x)
-  uint32_t x, kp, c, d;          // neighbour, position of u in N(x), #common, deg(x)
+constexpr int GW_BS_INLINE_BITS = 320;  // bitsets of deg(x) <= this live inside the entry
+constexpr int GW_BS_LIST = 20;          // <= this many common neighbours: sorted u16 positions inline
+struct gw_bs_nbr {  // GW_N2V_BITSET: one 64 B entry (one HBM sector) per adjacency slot (u -> x)
+  uint32_t x, d;                 // neighbour, deg(x)
   uint32_t off_lo, off_hi;       // offsets[x]
-  uint32_t roff_lo, roff_hi;     // word offset of the edge's bitset region
+  uint32_t kp, c;                // position of u in N(x), #common neighbours
+  uint32_t w[10];                // payload, by (c, d): c <= 20 && d < 65536: positions of the
+                                 // common neighbours (u16, ascending, 0xFFFF padded); else
+                                 // d <= 320: the bitset itself; else w[0..1] = region word offset
 };
+#if defined(__HIPCC__)
+#define GW_HD __host__ __device__
+#else
+#define GW_HD
+#endif
+GW_HD inline bool gw_bs_is_list(uint32_t c, uint32_t d) { return c <= GW_BS_LIST && d < 65536u; }
+static_assert(sizeof(gw_bs_nbr) == 64, "bitset entry must be one 64 B sector");
 
 struct gw_dev_graph {
   int64_t n = 0, nnz = 0;
@@ -93,7 +105,8 @@ struct gw_graph {
   // naive SimRank workspace (gw_simrank.hip)
   double* sr_work = nullptr;   // m*m doubles (U = A S), m = non-isolated vertices
   double* sr_x = nullptr;      // m*m compact S when m < n (else the output is used)
-  uint32_t* sr_ent = nullptr;  // [nnz + pad] compact neighbour | head-of-row flag
+  uint32_t* sr_ent = nullptr;    // [nnz + pad] byte offset of the compact neighbour
+  uint16_t* sr_heads = nullptr;  // [(nnz + pad) / 16] head-of-row bits
   int64_t* sr_off = nullptr;   // [m+1] compact offsets
   int32_t* sr_rows = nullptr;  // [m] compact id -> vertex
   int64_t sr_n = 0, sr_m = 0;

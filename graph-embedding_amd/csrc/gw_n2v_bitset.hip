@@ -18,14 +18,15 @@
 //                              bitset: expected d/(d-1-c) ~ 1 trial)
 //
 // Per edge slot s = (u -> v):
-//   bs_nbr[s] (32 B, one line): v, kp (position of u in N(v)), c, d = deg(v),
-//            offsets[v] (int64), region word offset (u64)
-//   region   dir[ndir]  cumulative set bits before each 512-bit block
-//                       (d > 512 only), then
+//   bs_nbr[s] (64 B, one HBM sector): v, d = deg(v), offsets[v] (int64),
+//            kp (position of u in N(v)), c, and either the bitset itself
+//            (d <= 320, inline) or the word offset of its region
+//   region   (d > 320 only) dir[ndir]  cumulative set bits before each
+//                       512-bit block (d > 512 only), then
 //            bits[ceil(d/32)]  bit k = (N(v)[k] != u) && has_edge(N(v)[k], u)
 // The entry chosen by a step carries everything the next step needs, so a
-// step touches ~2 lines (the chosen entry, one bitset word) instead of ~7 for
-// rejection sampling.
+// step into a vertex of degree <= 320 touches ONE random sector (the entry);
+// larger degrees add the bitset word (~2 sectors, vs ~7 for rejection).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -37,14 +38,17 @@
 namespace {
 
 constexpr int kB = 256;
-constexpr int kHdr = 0;          // no in-region header (metadata lives in bs_nbr)
+constexpr int kBlk = 16;         // words per 512-bit block: regions, directory and bits are block-aligned
 constexpr int kDirBits = 512;    // bits per directory block
 constexpr int kSmallD = 32;      // thread-per-slot fill up to this degree
 constexpr int kStage = 16;
 
 __host__ __device__ __forceinline__ int64_t bs_ndir(int64_t d) { return d > kDirBits ? (d + kDirBits - 1) / kDirBits : 0; }
+__host__ __device__ __forceinline__ int64_t bs_round(int64_t w) { return (w + kBlk - 1) / kBlk * kBlk; }
+// word offset of the bits inside a region (the directory is padded to a block)
+__host__ __device__ __forceinline__ int64_t bs_boff(int64_t d) { return d <= GW_BS_INLINE_BITS ? 0 : bs_round(bs_ndir(d)); }
 __host__ __device__ __forceinline__ int64_t bs_words(int64_t d) {
-  return kHdr + bs_ndir(d) + (d + 31) / 32;
+  return d <= GW_BS_INLINE_BITS ? 0 : bs_boff(d) + bs_round((d + 31) / 32);
 }
 
 __device__ __forceinline__ int32_t row_of_slot(const int64_t* __restrict__ off, int64_t n, int64_t e) {
@@ -66,6 +70,21 @@ __device__ __forceinline__ bool bs_has_edge(const gw_dev_graph& G, int64_t rb, i
     if (!((G.bitmap[bit >> 5] >> (bit & 31)) & 1u)) return false;
   }
   return gw_row_find(G.nbrs, rb, re, key) >= 0;
+}
+
+// position of the j-th (0-based) set bit of x (j < popc(x))
+__device__ __forceinline__ int word_select(uint32_t x, uint32_t j) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 16; w >= 1; w >>= 1) {
+    const uint32_t lowc = (uint32_t)__popc(x & ((1u << w) - 1u));
+    if (j >= lowc) {
+      j -= lowc;
+      x >>= w;
+      pos += w;
+    }
+  }
+  return pos;
 }
 
 __global__ void k_bs_sizes(int64_t nnz, const int32_t* __restrict__ nbrs, const int32_t* __restrict__ deg,
@@ -91,8 +110,12 @@ __global__ void k_bs_fill_small(gw_dev_graph G, const uint64_t* __restrict__ rof
   en.d = (uint32_t)d;
   en.off_lo = (uint32_t)(uint64_t)vb;
   en.off_hi = (uint32_t)((uint64_t)vb >> 32);
-  en.roff_lo = (uint32_t)R;
-  en.roff_hi = (uint32_t)(R >> 32);
+#pragma unroll
+  for (int t = 0; t < 10; ++t) en.w[t] = 0;
+  if (d > GW_BS_INLINE_BITS) {
+    en.w[0] = (uint32_t)R;
+    en.w[1] = (uint32_t)(R >> 32);
+  }
   if (d > kSmallD) {
     bsn[e] = en;  // c, kp filled by k_bs_fill_wave
     big[atomicAdd(nbig, 1ull)] = e;
@@ -111,8 +134,15 @@ __global__ void k_bs_fill_small(gw_dev_graph G, const uint64_t* __restrict__ rof
     }
   }
   en.c = c;
+  if (gw_bs_is_list(c, (uint32_t)d)) {  // sorted positions, 0xFFFF padded
+    uint16_t* lp = reinterpret_cast<uint16_t*>(en.w);
+    for (int t = 0; t < 2 * 10; ++t) lp[t] = 0xFFFFu;
+    int t = 0;
+    for (uint32_t x = word; x; x &= x - 1) lp[t++] = (uint16_t)(__ffs(x) - 1);
+  } else {
+    en.w[0] = word;  // inline bitset (d <= 32)
+  }
   bsn[e] = en;
-  if (d > 0) reg[R] = word;  // ndir == 0, one word
 }
 
 // one wave per large slot: 64 neighbours per ballot
@@ -129,12 +159,14 @@ __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff
     const int32_t u = row_of_slot(G.offsets, G.n, e);
     const int64_t vb = G.offsets[v], d = G.offsets[v + 1] - vb;
     const int64_t ub = G.offsets[u], ue = G.offsets[u + 1];
-    uint32_t* h = reg + roff[e];
-    const int64_t ndir = bs_ndir(d);
-    uint32_t* dir = h + kHdr;
-    uint32_t* bits = h + kHdr + ndir;
+    const bool inl = d <= GW_BS_INLINE_BITS;
+    uint32_t* h = inl ? bsn[e].w : reg + roff[e];
+    const int64_t ndir = inl ? 0 : bs_ndir(d);
+    uint32_t* dir = h;
+    uint32_t* bits = h + bs_boff(d);
     uint32_t c = 0;
     int kp_local = -1;
+    int my_pos = 0xFFFF;  // lane t < GW_BS_LIST: position of the t-th common neighbour
     for (int64_t base = 0; base < d; base += 64) {
       const int64_t k = base + lane;
       bool bit = false;
@@ -146,6 +178,19 @@ __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff
           bit = bs_has_edge(G, ub, ue, x);
       }
       const unsigned long long m = __ballot(bit);
+      {
+        // lane t collects the t-th set bit overall when it falls in this ballot
+        const int pc = __popcll(m);
+        const int r = lane - (int)c;
+        int src = 0;
+        if (r >= 0 && r < pc) {
+          const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+          const int plo = __popc(lo);
+          src = r < plo ? word_select(lo, (uint32_t)r) : 32 + word_select(hi, (uint32_t)(r - plo));
+        }
+        const int got = __shfl((int)k, src, 64);
+        if (r >= 0 && r < pc && lane < GW_BS_LIST) my_pos = got;
+      }
       if (ndir && (base % kDirBits) == 0 && lane == 0) dir[base / kDirBits] = c;
       if (lane == 0) {
         bits[base / 32] = (uint32_t)m;
@@ -160,6 +205,10 @@ __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff
       const int src = __ffsll(km) - 1;
       kp = __shfl(kp_local, src, 64);
     }
+    if (gw_bs_is_list(c, (uint32_t)d)) {
+      __threadfence();  // inline bit words written above by lane 0 land first
+      if (lane < GW_BS_LIST) reinterpret_cast<uint16_t*>(bsn[e].w)[lane] = (uint16_t)my_pos;
+    }
     if (lane == 0) {
       bsn[e].c = c;
       bsn[e].kp = (uint32_t)kp;
@@ -167,43 +216,96 @@ __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff
   }
 }
 
-// j-th (0-based) set bit of the region's bitset
-__device__ __forceinline__ int64_t bs_select(const uint32_t* __restrict__ h, int64_t d, int64_t ndir, uint32_t j) {
-  const uint32_t* dir = h + kHdr;
-  const uint32_t* bits = h + kHdr + ndir;
-  int64_t w0 = 0;
-  if (ndir > 0) {
-    int64_t lo = 0, hi = ndir - 1;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi + 1) >> 1;
-      if (dir[mid] <= j)
-        lo = mid;
-      else
-        hi = mid - 1;
-    }
-    j -= dir[lo];
-    w0 = lo * (kDirBits / 32);
-  }
-  const int64_t nw = (d + 31) >> 5;
-  for (int64_t w = w0; w < nw; ++w) {
-    uint32_t x = bits[w];
-    const uint32_t pc = (uint32_t)__popc(x);
-    if (j < pc) {
-      for (;;) {
-        const int t = __ffs(x) - 1;
-        if (j == 0) return w * 32 + t;
-        x &= x - 1;
-        --j;
+// j-th set bit among `nw` words held in registers (constant indices only)
+template <int NW>
+__device__ __forceinline__ int regs_select(const uint32_t (&wd)[NW], uint32_t j) {
+  uint32_t x = 0;
+  int base = 0;
+  bool found = false;
+#pragma unroll
+  for (int t = 0; t < NW; ++t) {
+    const uint32_t pc = (uint32_t)__popc(wd[t]);
+    if (!found) {
+      if (j < pc) {
+        x = wd[t];
+        base = 32 * t;
+        found = true;
+      } else {
+        j -= pc;
       }
     }
-    j -= pc;
   }
-  return 0;  // unreachable for j < c
+  return base + word_select(x, j);
+}
+
+// j-th set bit of an inline bitset (entry words, 8 B aligned; L2-resident)
+__device__ __forceinline__ int64_t inl_select(const uint32_t* __restrict__ w, uint32_t j) {
+  uint32_t wd[10];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) {
+    const uint2 v = reinterpret_cast<const uint2*>(w)[t];
+    wd[2 * t] = v.x;
+    wd[2 * t + 1] = v.y;
+  }
+  return regs_select<10>(wd, j);
+}
+
+// j-th set bit of a region bitset (c set bits): the 512-bit block comes from
+// the directory by interpolation (set bits are spread over the row), then
+// the block is read as one 64 B sector and searched in registers
+__device__ __forceinline__ int64_t bs_select(const uint32_t* __restrict__ h, int64_t d, uint32_t c, uint32_t j) {
+  const int64_t ndir = bs_ndir(d);
+  int64_t g = 0;
+  if (ndir > 0) {
+    g = (int64_t)((uint64_t)j * (uint64_t)ndir / c);
+    if (g >= ndir) g = ndir - 1;
+    uint32_t lo = h[g];
+    uint32_t hi = g + 1 < ndir ? h[g + 1] : c;
+    while (lo > j) {
+      --g;
+      hi = lo;
+      lo = h[g];
+    }
+    while (hi <= j) {
+      ++g;
+      lo = hi;
+      hi = g + 1 < ndir ? h[g + 1] : c;
+    }
+    j -= lo;
+  }
+  const uint4* blk = reinterpret_cast<const uint4*>(h + bs_boff(d) + g * kBlk);
+  uint32_t wd[kBlk];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint4 v = blk[t];
+    wd[4 * t] = v.x;
+    wd[4 * t + 1] = v.y;
+    wd[4 * t + 2] = v.z;
+    wd[4 * t + 3] = v.w;
+  }
+  return g * kDirBits + regs_select<kBlk>(wd, j);
+}
+
+// pl[idx] for a per-lane idx without dynamic register indexing
+__device__ __forceinline__ uint32_t pick10(const uint32_t (&pl)[10], uint32_t idx) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int t = 0; t < 10; ++t) r |= pl[t] & (0u - (uint32_t)(idx == (uint32_t)t));
+  return r;
+}
+
+// k in the inline common-neighbour list (registers, constant indices)
+__device__ __forceinline__ bool list_has(const uint32_t (&pl)[10], uint32_t k) {
+  bool hit = false;
+#pragma unroll
+  for (int t = 0; t < 10; ++t) hit |= (pl[t] & 0xFFFFu) == k || (pl[t] >> 16) == k;
+  return hit;
 }
 
 struct BsParams {
   double a_p, a_q;
   uint32_t k0, k1, pk0, pk1;
+  uint32_t diag;  // timing experiments only (GW_DIAG_BS): 1 = no select, 2 = no membership test
 };
 
 __global__ void __launch_bounds__(kB)
@@ -227,9 +329,16 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
     stage[0] = cur;
     int len = 1;
     uint32_t trial = 0;
-    uint64_t R = 0;          // region of edge (prev -> cur)
+    // bitset of edge (prev -> cur): inside its entry (deg(cur) <= 320: the
+    // entry's sector is already in L2, so reading a word is an L2 hit) or in
+    // the region store
+    const uint32_t* h = nullptr;
     int64_t b = G.offsets[cur], d = G.offsets[cur + 1] - b;  // row of cur
-    uint32_t c = 0, kp = 0, ndir = 0;
+    uint32_t c = 0, kp = 0, boff = 0;
+    bool inl = true, lst = false;
+    uint32_t pl[10];  // entry payload: the common-neighbour list in list mode
+#pragma unroll
+    for (int t = 0; t < 10; ++t) pl[t] = 0xFFFFFFFFu;
     while (len < L) {
       if (d == 0) break;
       int64_t k;
@@ -246,30 +355,43 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
         } else if (r - P.a_p < (double)c) {
           uint32_t j = (uint32_t)(r - P.a_p);
           if (j >= c) j = c - 1;
-          k = bs_select(G.bs_region + R, d, ndir, j);
+          k = (P.diag & 1) ? (int64_t)((uint64_t)j * (uint64_t)d / c)
+              : lst        ? (int64_t)((pick10(pl, j >> 1) >> (16 * (j & 1))) & 0xFFFFu)
+              : inl        ? (int64_t)regs_select<10>(pl, j)
+                           : bs_select(h, d, c, j);
         } else {
           k = (int64_t)gw_bounded(u.y, (uint32_t)d);
-          const uint32_t word = G.bs_region[R + kHdr + ndir + (k >> 5)];
-          acc = (k != (int64_t)kp) && !((word >> (k & 31)) & 1u);
+          const bool common = (P.diag & 2) ? false
+                              : lst ? list_has(pl, (uint32_t)k)
+                              : inl ? ((pick10(pl, (uint32_t)(k >> 5)) >> (k & 31)) & 1u)
+                                    : ((h[boff + (k >> 5)] >> (k & 31)) & 1u);
+          acc = (k != (int64_t)kp) && !common;
         }
       } else {  // retry of the "other" branch
         k = (int64_t)gw_bounded(u.y, (uint32_t)d);
-        const uint32_t word = G.bs_region[R + kHdr + ndir + (k >> 5)];
-        acc = ((k != (int64_t)kp) && !((word >> (k & 31)) & 1u)) || trial >= (1u << 24);
+        const bool common = lst ? list_has(pl, (uint32_t)k)
+                            : inl ? ((pick10(pl, (uint32_t)(k >> 5)) >> (k & 31)) & 1u)
+                                  : ((h[boff + (k >> 5)] >> (k & 31)) & 1u);
+        acc = ((k != (int64_t)kp) && !common) || trial >= (1u << 24);
       }
       if (acc) {
         my_trials += trial;
         trial = 0;
-        const uint4* ep = reinterpret_cast<const uint4*>(G.bs_nbr + (b + k));
-        const uint4 e0 = ep[0], e1 = ep[1];  // one 32 B entry: next step's metadata
+        const gw_bs_nbr* en = G.bs_nbr + (b + k);
+        const uint4* ep = reinterpret_cast<const uint4*>(en);
+        const uint4 e0 = ep[0], e1 = ep[1], e2 = ep[2], e3 = ep[3];  // one 64 B entry: next step's state
         prev = cur;
         cur = (int32_t)e0.x;
-        kp = e0.y;
-        c = e0.z;
-        d = (int64_t)e0.w;
-        b = (int64_t)((uint64_t)e1.x | ((uint64_t)e1.y << 32));
-        R = (uint64_t)e1.z | ((uint64_t)e1.w << 32);
-        ndir = (uint32_t)bs_ndir(d);
+        d = (int64_t)e0.y;
+        b = (int64_t)((uint64_t)e0.z | ((uint64_t)e0.w << 32));
+        kp = e1.x;
+        c = e1.y;
+        lst = gw_bs_is_list(c, (uint32_t)d);
+        inl = !lst && d <= GW_BS_INLINE_BITS;
+        h = (lst || inl) ? en->w : G.bs_region + ((uint64_t)e1.z | ((uint64_t)e1.w << 32));
+        boff = (uint32_t)bs_boff(d);
+        pl[0] = e1.z; pl[1] = e1.w; pl[2] = e2.x; pl[3] = e2.y; pl[4] = e2.z;
+        pl[5] = e2.w; pl[6] = e3.x; pl[7] = e3.y; pl[8] = e3.z; pl[9] = e3.w;
         stage[64 * (len & (kStage - 1))] = cur;
         if ((len & (kStage - 1)) == kStage - 1) {
           int32_t* dst = row + (len - (kStage - 1));
@@ -361,6 +483,7 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes) {
   uint64_t words = 0;
   GW_HIP_TRY(hipMemcpy(&words, roff + nnz, sizeof(uint64_t), hipMemcpyDeviceToHost));
   const int64_t need = (int64_t)words * 4 + nnz * (int64_t)sizeof(gw_bs_nbr);
+  if (words == 0) words = 1;  // every bitset is inline: keep a valid region pointer
   if (need > budget_bytes) {
     bs_free(roff);
     g->err = "per-edge bitsets need " + std::to_string(need) + " B (sum(deg^2) bits); over the " +
@@ -401,6 +524,8 @@ int gw_dev_walk_bitset_launch(gw_graph* g, int L, uint64_t seed, int64_t walk_be
   P.k1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_STEP;
   P.pk0 = (uint32_t)seed;
   P.pk1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_PERM;
+  const char* dg = getenv("GW_DIAG_BS");  // diagnostic A/B knob only
+  P.diag = dg ? (uint32_t)atoi(dg) : 0u;
   const unsigned grid = (unsigned)std::max<int64_t>(1, (walk_count + kB - 1) / kB);
   k_walk_bitset<<<grid, kB, 0, (hipStream_t)stream>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev,
                                                        len_dev, (unsigned long long*)counters_dev);

@@ -36,11 +36,10 @@ namespace {
 
 constexpr int SR_BLOCK = 1024;
 constexpr int SR_WAVES = SR_BLOCK / 64;
-constexpr int SR_K = 8;                          // adjacency entries per lane per chunk
+constexpr int SR_K = 16;                         // adjacency entries per lane per chunk
 constexpr int SR_CHUNK = 64 * SR_K;              // entries per wave per chunk
 constexpr int64_t SR_LDS_BYTES = 152 * 1024;     // dynamic LDS per workgroup (input row + window)
 constexpr int64_t SR_MIN_WIN = 2048;             // smallest output window (rows)
-constexpr uint32_t SR_HEAD = 0x80000000u;        // entry is the first of its row
 
 // The passes run over the compact graph of the m non-isolated vertices
 // (isolated rows/columns of SimRank are 0): compact ids are consecutive, so
@@ -49,7 +48,8 @@ constexpr uint32_t SR_HEAD = 0x80000000u;        // entry is the first of its ro
 struct SrArgs {
   int64_t m;
   const int64_t* off;   // [m+1] compact CSR offsets
-  const uint32_t* ent;  // [nnz + pad] compact neighbour | SR_HEAD
+  const uint32_t* ent;    // [nnz + pad] byte offset (8 * compact neighbour) into a row
+  const uint16_t* heads;  // [(nnz + pad) / 16] bit k of word g: entry 16g+k starts a row
   double C;
 };
 
@@ -163,31 +163,34 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_gather(SrArgs A, const double* 
       if (eb < ee) {
         const int64_t base0 = eb & ~(int64_t)(SR_K - 1);
         const uint32_t* ep = A.ent + base0 + SR_K * lane;
+        const uint16_t* hp = A.heads + base0 / SR_K + lane;
         const int pb = (int)(eb - base0);          // slice = chunk positions [pb, pe)
         const int pe = (int)(ee - base0);
         // the slice's first head flag is dropped: its row is cur_row from the start,
         // so every flag seen afterwards closes a row of this slice
         int cur_row = (int)(ra - j0);
         double chunk_carry = 0.0;
-        uint4 n0 = *reinterpret_cast<const uint4*>(ep);
-        uint4 n1 = *reinterpret_cast<const uint4*>(ep + 4);
+        uint4 n[4];
+        uint32_t nh;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) n[q] = *reinterpret_cast<const uint4*>(ep + 4 * q);
+        nh = *hp;
         for (int pos = 0; pos < pe; pos += SR_CHUNK) {
-          const uint32_t en[SR_K] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
+          const uint32_t en[SR_K] = {n[0].x, n[0].y, n[0].z, n[0].w, n[1].x, n[1].y, n[1].z, n[1].w,
+                                     n[2].x, n[2].y, n[2].z, n[2].w, n[3].x, n[3].y, n[3].z, n[3].w};
+          uint32_t fl = nh;  // bit k: entry k starts a row
           if (pos + SR_CHUNK < pe) {
-            n0 = *reinterpret_cast<const uint4*>(ep + pos + SR_CHUNK);
-            n1 = *reinterpret_cast<const uint4*>(ep + pos + SR_CHUNK + 4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) n[q] = *reinterpret_cast<const uint4*>(ep + pos + SR_CHUNK + 4 * q);
+            nh = hp[(pos + SR_CHUNK) / SR_K];
           }
           const int p0 = pos + SR_K * lane;
           const bool full = pos > pb && pos + SR_CHUNK < pe;  // wave-uniform
           double x[SR_K];
-          uint32_t fl = 0;  // bit k: entry k starts a row
 #pragma unroll
-          for (int k = 0; k < SR_K; ++k) {
-            // every entry word (padding included) indexes inside the row: read unconditionally
-            const uint32_t b = en[k] & ~SR_HEAD;
-            x[k] = LDS_ROW ? in_row[b] : row[b];
-            fl |= (en[k] >> 31) << k;
-          }
+          for (int k = 0; k < SR_K; ++k)  // every entry word (padding included) is inside the row
+            x[k] = LDS_ROW ? *reinterpret_cast<const double*>(reinterpret_cast<const char*>(in_row) + en[k])
+                           : *reinterpret_cast<const double*>(reinterpret_cast<const char*>(row) + en[k]);
           if (!full) {
 #pragma unroll
             for (int k = 0; k < SR_K; ++k) {
@@ -200,30 +203,30 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_gather(SrArgs A, const double* 
           const int incl = add_scan(nf, lane);
           const int total = __builtin_amdgcn_readlane(incl, 63);
           const uint64_t headmask = __ballot(fl != 0);
-          // trailing-segment sum of the lane; lane 0 starts from the chunk carry
-          double agg = lane == 0 ? chunk_carry : 0.0;
-#pragma unroll
-          for (int k = 0; k < SR_K; ++k) {
-            if (fl & (1u << k)) agg = 0.0;
-            agg += x[k];
-          }
-          const uint64_t hb = headmask & below_incl;
-          const int seg_start = hb ? 63 - __builtin_clzll(hb) : 0;
-          const double S = seg_scan(agg, lane, seg_start);
-          const double prevS = dpp_f64<0x138>(S);  // wave_shr:1
-          double acc = lane == 0 ? chunk_carry : prevS;
-          int r = cur_row + incl - nf;
+          // lane-local walk: every row that ends inside the lane is written
+          // with its lane-local part; the lane's first such row gets the
+          // carry-in added after the scan
+          const int r0 = cur_row + incl - nf;
+          int r = r0;
+          double p = 0.0;
 #pragma unroll
           for (int k = 0; k < SR_K; ++k) {
             if (fl & (1u << k)) {
-              out_win[r] = acc;
+              out_win[r] = p;
               ++r;
-              acc = 0.0;
             }
-            acc += x[k];
+            p = ((fl & (1u << k)) ? 0.0 : p) + x[k];
           }
+          // p = the lane's trailing segment; lane 0 without a head continues the chunk carry
+          if (lane == 0 && fl == 0) p = chunk_carry + p;
+          const uint64_t hb = headmask & below_incl;
+          const int seg_start = hb ? 63 - __builtin_clzll(hb) : 0;
+          const double S = seg_scan(p, lane, seg_start);
+          const double prevS = dpp_f64<0x138>(S);  // wave_shr:1
+          const double carry_in = lane == 0 ? chunk_carry : prevS;
+          if (fl) out_win[r0] = carry_in + out_win[r0];
           // the lane holding the slice's last entry writes that row (x = 0 past it)
-          if (!full && p0 <= pe - 1 && pe - 1 < p0 + SR_K) out_win[r] = acc;
+          if (!full && p0 <= pe - 1 && pe - 1 < p0 + SR_K) out_win[r] = S;
           const uint64_t Sb = __double_as_longlong(S);
           chunk_carry = __longlong_as_double(
               (long long)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(Sb >> 32), 63) << 32) |
@@ -273,6 +276,7 @@ void gw_dev_simrank_release(gw_graph* g) {
   sr_free(g->sr_work);
   sr_free(g->sr_x);
   sr_free(g->sr_ent);
+  sr_free(g->sr_heads);
   sr_free(g->sr_off);
   sr_free(g->sr_rows);
   g->sr_n = 0;
@@ -294,9 +298,11 @@ static int sr_build_layout(gw_graph* g) {
       off.push_back(g->offsets[v + 1]);
     }
   std::vector<uint32_t> ent((size_t)padded, 0);
+  std::vector<uint16_t> heads((size_t)(padded / SR_K), 0);
   for (int64_t v = 0; v < n; ++v) {
     const int64_t b = g->offsets[v], e = g->offsets[v + 1];
-    for (int64_t k = b; k < e; ++k) ent[k] = (uint32_t)rank[g->nbrs[k]] | (k == b ? SR_HEAD : 0u);
+    if (e > b) heads[(size_t)(b / SR_K)] |= (uint16_t)(1u << (b % SR_K));
+    for (int64_t k = b; k < e; ++k) ent[k] = (uint32_t)rank[g->nbrs[k]] * (uint32_t)sizeof(double);
   }
   auto up = [&](auto*& dptr, const auto& vec) -> bool {
     const size_t bytes = std::max<size_t>(vec.size() * sizeof(vec[0]), 16);
@@ -307,7 +313,7 @@ static int sr_build_layout(gw_graph* g) {
     }
     return vec.empty() || hipMemcpy(dptr, vec.data(), vec.size() * sizeof(vec[0]), hipMemcpyHostToDevice) == hipSuccess;
   };
-  if (!up(g->sr_ent, ent) || !up(g->sr_off, off) || !up(g->sr_rows, rows)) {
+  if (!up(g->sr_ent, ent) || !up(g->sr_heads, heads) || !up(g->sr_off, off) || !up(g->sr_rows, rows)) {
     g->err = "naive SimRank adjacency layout does not fit in device memory";
     return GW_ERR_NOMEM;
   }
@@ -345,7 +351,7 @@ int gw_dev_simrank_naive(gw_graph* g, double C, int iters, double* sim_dev, void
     const unsigned mbk = (unsigned)((m + 255) / 256);
     k_sr_identity<<<mbk, 256, 0, s>>>(m, X);
     GW_HIP_TRY(hipGetLastError());
-    SrArgs A{m, g->sr_off, g->sr_ent, C};
+    SrArgs A{m, g->sr_off, g->sr_ent, g->sr_heads, C};
     // input row in LDS when it leaves room for a window of SR_MIN_WIN rows;
     // GW_DIAG_SR_GLOBAL_ROW=1 forces the HBM-row variant (tests compare the two)
     const char* diag = std::getenv("GW_DIAG_SR_GLOBAL_ROW");
