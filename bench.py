@@ -23,7 +23,9 @@ Also reported (same JSON line):
   cpu_baseline  the oracle's C restatement of the same sampling (OpenMP),
                 timed on a bounded sample of the same workload (rank 0, N=1).
   secondary     TopSim_singleSample on lshrank blog (STEP=5, SAMPLE=10000,
-                C=0.6, top-20, all 10,313 sources): pair-updates/s.
+                C=0.6, top-20, all 10,313 sources): pair-updates/s; and
+                secondary.simrank_naive: SimRank.java (STEP=3, C=0.6) on blog,
+                dense 10,313^2 fp64 result: rounds/s, LDS-gather roofline.
 """
 import argparse
 import json
@@ -58,6 +60,9 @@ def parse():
     ap.add_argument("--mode", choices=["auto", "bitset", "rejection"], default="auto",
                     help="second-order sampler (auto: bitset when it fits in HBM)")
     ap.add_argument("--no-topsim", action="store_true")
+    ap.add_argument("--no-simrank", action="store_true")
+    ap.add_argument("--simrank-graph", default="blog", help="naive SimRank graph (blog or moreno)")
+    ap.add_argument("--simrank-rounds", type=int, default=3, help="SimRank.java STEP")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--topsim-sample", type=int, default=10000)
@@ -357,6 +362,67 @@ def main():
         secondary = res[0]
         if len(res) > 1:
             secondary["more"] = res[1:]
+
+    # ---- naive SimRank (SimRank.java) on the GPU: the TopSim ground truth ----
+    def run_simrank(name):
+        from gwamd import topsim
+        fname, V, sep, desc = TOPSIM_GRAPHS[name]
+        tg = topsim.Graph(os.path.join(ROOT, "tests", "golden", "data", fname), V, separator=sep,
+                          device=dev.index)
+        tg._ensure_device()
+        h = tg._g.handle
+        rounds = args.simrank_rounds
+        S = torch.empty((V, V), dtype=torch.float64, device=dev)
+        C.check(C.lib().gw_simrank_naive(h, 0.6, rounds, C.ptr(S), sh), h)  # warm-up, workspace
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        C.check(C.lib().gw_simrank_naive(h, 0.6, rounds, C.ptr(S), sh), h)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        sec = e0.elapsed_time(e1) * 1e-3
+        deg = np.diff(tg._offs)
+        nnz = int(deg.sum())
+        m = int((deg > 0).sum())
+        # entry gathers of the two passes (pass 1: m*nnz, pass 2: rows j > i only)
+        tail = np.cumsum(deg[::-1])[::-1]  # entries of rows >= v
+        p2 = int(tail[1:][deg[:-1] > 0].sum())
+        gathers = rounds * (m * nnz + p2)
+        lds_peak = 128.0 / 8 * 256 * 2.4e9  # 8 B gathers at 128 B/clk/CU
+        java_pairs = (nnz * nnz - int((deg.astype(np.int64) ** 2).sum())) // 2
+        cpu_sr = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            import oracle
+            nth = min(16, os.cpu_count() or 1)
+            budget, acc, re_ = 1.2e11, 0, 1
+            suffix = nnz - np.cumsum(deg)
+            while re_ < V and acc < budget:
+                acc += int(deg[re_]) * int(suffix[re_])
+                re_ += 1
+            Sh = np.eye(V)
+            t0 = time.perf_counter()
+            _, pairs = oracle.simrank_round_rows(tg._offs, tg._nbrs, 0.6, Sh, 1, re_, nthreads=nth)
+            dt = time.perf_counter() - t0
+            cpu_sr = {"value": pairs / dt / java_pairs, "unit": "rounds/s", "cores": nth, "kind": "port",
+                      "sample": f"rows 1..{re_ - 1} of one round ({pairs} neighbour pairs, {dt:.1f} s), "
+                                f"oracle/oracle.c or_simrank_round_rows (SimRank.java loop order), "
+                                f"scaled by the round's {java_pairs} pairs"}
+        return {
+            "metric": "naive SimRank rounds/sec (SimRank.java)", "value": rounds / sec, "unit": "rounds/s",
+            "config": {"workload": f"SimRank(g).compute() on {name} ({desc}, Java multigraph)",
+                       "rounds": rounds, "C": 0.6, "dense_result": f"{V}x{V} fp64"},
+            "seconds": sec, "entry_gathers": gathers, "java_neighbour_pairs_per_round": java_pairs,
+            "roofline": {"bound": "lds", "achieved": gathers / sec, "peak": lds_peak, "unit": "gathers/s",
+                         "frac": gathers / sec / lds_peak, "traffic": None, "kernel": "k_sr_gather<true,*>"},
+            "cpu_baseline": cpu_sr,
+        }
+
+    if not args.no_simrank:
+        sr = run_simrank(args.simrank_graph)
+        if secondary is None:
+            secondary = {"simrank_naive": sr}
+        else:
+            secondary["simrank_naive"] = sr
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

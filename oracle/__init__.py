@@ -51,6 +51,8 @@ def lib():
         L.or_walks_bitset.argtypes = [i64, v, v, v, d, d, u64, ci, i64, i64, ci, v, v, v, ci]
         L.or_topsim.argtypes = [i64, v, v, ci, ci, ci, d, u64, ci, i64, v, i64, v, v, ci]
         L.or_simrank_naive.argtypes = [i64, v, v, d, ci, v, ci]
+        L.or_simrank_round_rows.argtypes = [i64, v, v, d, v, i64, i64, v, ci]
+        L.or_simrank_round_rows.restype = i64
         _lib = L
     return _lib
 
@@ -181,6 +183,18 @@ def simrank_naive(offsets, nbrs, C, iters, nthreads=0):
     sim = np.zeros((n, n), np.float64)
     lib().or_simrank_naive(n, _p(off), _p(nb), float(C), int(iters), _p(sim), int(nthreads))
     return sim
+
+
+def simrank_round_rows(offsets, nbrs, C, S, rb, re, nthreads=0):
+    """One SimRank.java sweep for rows [rb, re) from matrix S -> (rows, pairs)."""
+    off = np.ascontiguousarray(offsets, np.int64)
+    nb = np.ascontiguousarray(nbrs, np.int32)
+    n = len(off) - 1
+    S = np.ascontiguousarray(S, np.float64)
+    out = np.zeros((re - rb, n), np.float64)
+    pairs = lib().or_simrank_round_rows(n, _p(off), _p(nb), float(C), _p(S), int(rb), int(re), _p(out),
+                                        int(nthreads))
+    return out, int(pairs)
 
 
 # ---- pure-Python restatements ---------------------------------------------------

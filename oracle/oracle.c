@@ -572,6 +572,32 @@ void or_simrank_naive(int64_t n, const int64_t* off, const int32_t* nbrs, double
   free(tmp);
 }
 
+/* One sweep of SimRank.java:42-47 for rows [rb, re) only (timing samples   */
+/* for bench.py's CPU baseline): out[(i-rb)*n + j] = sim(i, j), j > i, from */
+/* the matrix S.  Returns the number of neighbour pairs summed.             */
+int64_t or_simrank_round_rows(int64_t n, const int64_t* off, const int32_t* nbrs, double C, const double* S,
+                              int64_t rb, int64_t re, double* out, int nthreads) {
+  int64_t pairs = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : pairs)
+#endif
+  for (int64_t i = rb; i < re; ++i)
+    for (int64_t j = i + 1; j < n; ++j) {
+      double v = 0.0;
+      int64_t di = off[i + 1] - off[i], dj = off[j + 1] - off[j];
+      if (di != 0 && dj != 0) {
+        double res = 0.0;
+        for (int64_t a = off[i]; a < off[i + 1]; ++a)
+          for (int64_t b = off[j]; b < off[j + 1]; ++b) res += S[(int64_t)nbrs[a] * n + nbrs[b]];
+        v = C * res / (double)(di * dj);
+        pairs += di * dj;
+      }
+      out[(i - rb) * n + j] = v;
+    }
+  return pairs;
+}
+
 /* ------------------------------------------------------------------------ */
 /* GW_N2V_BITSET restatement: the same 3-way exact mixture of the reference */
 /* get_alias_edge weights (node2vec.py:61-81; unweighted, undirected), but   */
