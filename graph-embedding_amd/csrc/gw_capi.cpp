@@ -24,6 +24,9 @@ int gw_write_sim_dense_impl(const char* path, const double* rows, const int32_t*
 int gw_write_sim_topk_impl(const char* path, const int32_t* ids, const double* scores,
                            const int32_t* row_ids, int64_t nrows, int topk,
                            const std::string& sep, int decimals, std::string* err);
+int gw_write_sim_cachemap_impl(const char* path, const int32_t* keys, const float* vals, const int32_t* sizes,
+                               const int32_t* row_ids, int64_t nrows, int capacity, int topk,
+                               const std::string& sep, std::string* err);
 int gw_hip_device_count(int* count);
 
 static thread_local std::string tls_err;
@@ -326,6 +329,17 @@ int gw_topsim_dense(gw_graph* g, int variant, int sample, int step, double C, ui
                               out_rows_dev, stats_dev, stream));
 }
 
+int gw_topsim_m(gw_graph* g, int variant, int capacity, int sample, int step, double C, uint64_t seed,
+                const int32_t* sources_dev, int64_t nsrc, int32_t* out_keys_dev, float* out_vals_dev,
+                int32_t* out_size_dev, int64_t* stats_dev, void* stream) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  if (g->device < 0) return ret(g, gw_fail(g, GW_ERR_STATE, "graph is not on a device"));
+  if (nsrc < 0 || capacity < 1 || (nsrc > 0 && (!sources_dev || !out_keys_dev || !out_vals_dev || !out_size_dev)))
+    return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
+  return ret(g, gw_dev_topsim_m(g, variant, capacity, sample, step, C, seed, sources_dev, nsrc, out_keys_dev,
+                                out_vals_dev, out_size_dev, stats_dev, stream));
+}
+
 int gw_simrank_naive(gw_graph* g, double C, int iters, double* sim_dev, void* stream) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
   if (g->device < 0) return ret(g, gw_fail(g, GW_ERR_STATE, "graph is not on a device"));
@@ -363,6 +377,18 @@ int gw_write_sim_text_topk(const char* path, const int32_t* ids, const double* s
     return gw_fail(nullptr, GW_ERR_INVALID, "bad arguments");
   std::string err;
   int rc = gw_write_sim_topk_impl(path, ids, scores, row_ids, nrows, topk, sep ? sep : ",", decimals, &err);
+  if (rc != GW_OK) return gw_fail(nullptr, rc, "%s", err.c_str());
+  return GW_OK;
+}
+
+int gw_write_sim_text_cachemap(const char* path, const int32_t* keys, const float* vals, const int32_t* sizes,
+                               const int32_t* row_ids, int64_t nrows, int capacity, int topk, const char* sep) {
+  if (!path || (nrows > 0 && (!keys || !vals || !sizes)) || capacity < 1 || topk < 0)
+    return gw_fail(nullptr, GW_ERR_INVALID, "bad arguments");
+  for (int64_t r = 0; r < nrows; ++r)
+    if (sizes[r] < 0 || sizes[r] > capacity) return gw_fail(nullptr, GW_ERR_INVALID, "row size outside [0, capacity]");
+  std::string err;
+  int rc = gw_write_sim_cachemap_impl(path, keys, vals, sizes, row_ids, nrows, capacity, topk, sep ? sep : ",", &err);
   if (rc != GW_OK) return gw_fail(nullptr, rc, "%s", err.c_str());
   return GW_OK;
 }

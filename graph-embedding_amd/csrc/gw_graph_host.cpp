@@ -740,3 +740,38 @@ int gw_write_sim_topk_impl(const char* path, const int32_t* ids, const double* s
   if (rc != GW_OK) *err = "write failed";
   return rc;
 }
+
+// Print.printByOrder(FixedCacheMap[] sim, outPath, topk) (Print.java:94-124):
+// each row iterates its map ascending and prints the last `topk` entries,
+// "%.6f" of the float value (Formatter widens the float to double).
+int gw_write_sim_cachemap_impl(const char* path, const int32_t* keys, const float* vals, const int32_t* sizes,
+                               const int32_t* row_ids, int64_t nrows, int capacity, int topk,
+                               const std::string& sep, std::string* err) {
+  std::string p2 = std::string(path) + ".sim.txt";
+  FILE* f1 = fopen(path, "wb");
+  FILE* f2 = fopen(p2.c_str(), "wb");
+  if (!f1 || !f2) {
+    if (f1) fclose(f1);
+    if (f2) fclose(f2);
+    *err = std::string("cannot open '") + path + "'";
+    return GW_ERR_IO;
+  }
+  std::vector<std::string> o(nrows), os(nrows);
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t r = 0; r < nrows; ++r) {
+    std::vector<JPair> row;
+    const int size = sizes[r];
+    for (int i = std::max(0, size - topk); i < size; ++i)
+      row.push_back(JPair{keys[r * (int64_t)capacity + i], (double)vals[r * (int64_t)capacity + i]});
+    emit_row(o[r], os[r], row_ids ? row_ids[r] : r, row, sep, 6);
+  }
+  int rc = GW_OK;
+  for (int64_t r = 0; r < nrows; ++r) {
+    if (fwrite(o[r].data(), 1, o[r].size(), f1) != o[r].size()) rc = GW_ERR_IO;
+    if (fwrite(os[r].data(), 1, os[r].size(), f2) != os[r].size()) rc = GW_ERR_IO;
+  }
+  if (fclose(f1) != 0) rc = GW_ERR_IO;
+  if (fclose(f2) != 0) rc = GW_ERR_IO;
+  if (rc != GW_OK) *err = "write failed";
+  return rc;
+}

@@ -135,6 +135,9 @@ int gw_dev_n2v_walks_replay(gw_graph* g, int walk_len, int64_t nwalks,
                             int32_t* out_len, int64_t* uniforms_used);
 void gw_dev_bitset_release(gw_graph* g);
 void gw_dev_simrank_release(gw_graph* g);
+int gw_dev_topsim_m(gw_graph* g, int variant, int capacity, int sample, int step, double C, uint64_t seed,
+                    const int32_t* sources_dev, int64_t nsrc, int32_t* out_keys_dev, float* out_vals_dev,
+                    int32_t* out_size_dev, int64_t* stats_dev, void* stream);
 int gw_dev_simrank_naive(gw_graph* g, double C, int iters, double* sim_dev, void* stream);
 int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes);
 int gw_dev_walk_bitset_launch(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int64_t walk_count,

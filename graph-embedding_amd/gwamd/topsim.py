@@ -158,6 +158,90 @@ class SingleRandomWalk(_TopSimBase):
     VARIANT = C.TOPSIM_SINGLE_RW
 
 
+class FixedCacheMap:
+    """lxctools.FixedCacheMap contents as produced on the GPU: the entries in
+    iteration order (ascending value, FixedCacheMap.java:104-127).  Iterating
+    empties it, as the Java iterator does (delMin)."""
+
+    def __init__(self, keys, vals, capacity):
+        self._items = [(int(k), float(v)) for k, v in zip(keys, vals)]
+        self.NMAX = int(capacity)
+
+    def size(self):
+        return len(self._items)
+
+    def isEmpty(self):
+        return not self._items
+
+    def __iter__(self):
+        while self._items:
+            yield self._items.pop(0)
+
+
+class _TopSimM:
+    """Shared by TopSim_singleSample_M / SingleRandomWalk_M (STEP = 5 as in
+    the reference; `step` overrides it)."""
+    VARIANT = C.TOPSIM_SINGLE_SAMPLE
+    STEP = 5
+
+    def __init__(self, g, M, sample, C_=C_DEFAULT, seed=0, step=None, topk=TOPK):
+        self.g = g
+        self.COUNT = g.getVCount()
+        self.capacity = int(topk) * int(M)  # capacity = topk * M (:37)
+        self.SAMPLE = int(sample)
+        self.STEP = type(self).STEP if step is None else int(step)
+        self.C = float(C_)
+        self.seed = int(seed)
+        self.stats = None
+        self._raw = None
+
+    def compute(self, sources=None):
+        import torch
+        g = self.g
+        g._ensure_device()
+        dev = torch.device("cuda", g.device)
+        src_np = np.arange(self.COUNT, dtype=np.int32) if sources is None else np.asarray(sources, np.int32)
+        src = torch.as_tensor(src_np, device=dev)
+        cap = self.capacity
+        keys = torch.empty((len(src), cap), dtype=torch.int32, device=dev)
+        vals = torch.empty((len(src), cap), dtype=torch.float32, device=dev)
+        size = torch.empty(len(src), dtype=torch.int32, device=dev)
+        st = torch.zeros(4, dtype=torch.int64, device=dev)
+        h = g._g.handle
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        C.check(C.lib().gw_topsim_m(h, self.VARIANT, cap, self.SAMPLE, self.STEP, self.C, self.seed,
+                                    C.ptr(src), len(src), C.ptr(keys), C.ptr(vals), C.ptr(size), C.ptr(st),
+                                    stream), h)
+        s = st.cpu().numpy()
+        self.stats = dict(extensions=int(s[0]), pair_updates=int(s[1]), max_frontier=int(s[2]),
+                          walkers=int(s[3]))
+        self._raw = (src_np, keys.cpu().numpy(), vals.cpu().numpy(), size.cpu().numpy())
+
+    def raw(self):
+        """(sources, keys[nsrc, capacity], values float32, sizes) in iteration order."""
+        if self._raw is None:
+            raise RuntimeError("call compute() first")
+        return self._raw
+
+    def getResult(self):
+        """FixedCacheMap[] (one per vertex; rows not computed are empty)."""
+        src, keys, vals, size = self.raw()
+        out = [FixedCacheMap([], [], self.capacity) for _ in range(self.COUNT)]
+        for r, v in enumerate(src):
+            out[int(v)] = FixedCacheMap(keys[r, :size[r]], vals[r, :size[r]], self.capacity)
+        return out
+
+
+class TopSim_singleSample_M(_TopSimM):
+    """simrank.TopSim_singleSample_M (TopSim_singleSample_M.java:21-243)."""
+    VARIANT = C.TOPSIM_SINGLE_SAMPLE
+
+
+class SingleRandomWalk_M(_TopSimM):
+    """simrank.SingleRandomWalk_M (SingleRandomWalk_M.java:15-102)."""
+    VARIANT = C.TOPSIM_SINGLE_RW
+
+
 class SimRank:
     """simrank.SimRank (SimRank.java:15-82): naive SimRank, STEP = 3 rounds
     (the reference's private field; `step` overrides it), C from
@@ -215,7 +299,16 @@ def printByOrderAll(sim, outPath, topk=1000, testTopK=10, separator=SEPARATOR):
 def printByOrder(sim, outPath, topk=TOPK, testTopK=None, separator=SEPARATOR, decimals=6):
     """Print.printByOrder (Print.java:25-53): `outPath` gets "v,id,...\\r\\n" and
     `outPath.sim.txt` gets "v,id:%.6f,...\\r\\n".  `sim` is a dense V x V array
-    (exact Java FixedMaxPQ tie order and %.6f HALF_UP) or a TopSim object."""
+    (exact Java FixedMaxPQ tie order and %.6f HALF_UP), a TopSim object, or a
+    TopSim_M object (the FixedCacheMap[] overload, Print.java:94-124: last
+    `topk` entries of each map's ascending iteration)."""
+    if isinstance(sim, _TopSimM):
+        src, keys, vals, size = sim.raw()
+        C.check(C.lib().gw_write_sim_text_cachemap(
+            str(outPath).encode(), C.ptr(np.ascontiguousarray(keys)), C.ptr(np.ascontiguousarray(vals)),
+            C.ptr(np.ascontiguousarray(size)), C.ptr(np.ascontiguousarray(src, np.int32)), keys.shape[0],
+            keys.shape[1], int(topk), separator.encode()))
+        return
     if isinstance(sim, _TopSimBase):
         if sim._rows is not None:
             rows, ids = sim._rows, sim._sources

@@ -99,6 +99,23 @@ void TopSimBase::topK(int k, std::vector<int32_t>& ids, std::vector<double>& sco
             g_.handle());
 }
 
+void TopSimM::compute() {
+  const int64_t V = g_.getVCount();
+  std::vector<int32_t> src((size_t)V);
+  for (int64_t i = 0; i < V; ++i) src[(size_t)i] = (int32_t)i;
+  keys_.assign((size_t)(V * capacity), -1);
+  vals_.assign((size_t)(V * capacity), 0.f);
+  sizes_.assign((size_t)V, 0);
+  int64_t st[4] = {0, 0, 0, 0};
+  gw::check(gw_topsim_m_host(g_.handle(), variant_, capacity, SAMPLE, STEP, conf::MyConfiguration::C, seed_,
+                             src.data(), V, keys_.data(), vals_.data(), sizes_.data(), st),
+            g_.handle());
+  stats_.extensions = st[0];
+  stats_.pair_updates = st[1];
+  stats_.max_frontier = st[2];
+  stats_.walkers = st[3];
+}
+
 void SimRank::compute() {
   const int64_t V = g_.getVCount();
   sim_.assign((size_t)(V * V), 0.0);
@@ -135,6 +152,14 @@ void Print::printByOrder(const simrank::TopSimBase& sim, const std::string& outP
 void Print::printByOrder(const std::vector<double>& sim, int64_t V, const std::string& outPath, int topk, int) {
   gw::check(gw_write_sim_text_dense(outPath.c_str(), sim.data(), nullptr, (int64_t)(sim.size() / V), V, topk,
                                     conf::MyConfiguration::SEPARATOR.c_str(), 6));
+}
+
+void Print::printByOrder(const simrank::TopSimM& sim, const std::string& outPath, int topk) {
+  std::vector<int32_t> sizes((size_t)sim.getVCount());
+  for (int v = 0; v < sim.getVCount(); ++v) sizes[(size_t)v] = sim.size(v);
+  gw::check(gw_write_sim_text_cachemap(outPath.c_str(), sim.keys().data(), sim.values().data(), sizes.data(),
+                                       nullptr, sim.getVCount(), sim.getCapacity(), topk,
+                                       conf::MyConfiguration::SEPARATOR.c_str()));
 }
 
 void Print::printByOrderAll(const std::vector<double>& sim, int64_t V, const std::string& outPath, int topk, int) {

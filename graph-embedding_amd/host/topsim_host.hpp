@@ -121,6 +121,38 @@ class SingleRandomWalk : public TopSimBase {
       : TopSimBase(g, sample, step, GW_TOPSIM_SINGLE_RW, seed) {}
 };
 
+// simrank.TopSim_singleSample_M / SingleRandomWalk_M: FixedCacheMap rows
+// (capacity = TOPK * M), iteration order (ascending), STEP = 5 as the reference.
+class TopSimM {
+ public:
+  TopSimM(structures::Graph& g, int M, int sample, int variant, uint64_t seed, int step)
+      : g_(g), capacity(conf::MyConfiguration::TOPK * M), SAMPLE(sample), STEP(step), variant_(variant), seed_(seed) {}
+  void compute();  // every vertex
+  int getCapacity() const { return capacity; }
+  int getVCount() const { return g_.getVCount(); }
+  // row v: size(v) entries keys()[v*capacity + i], values()[...] ascending
+  int size(int v) const { return sizes_[v]; }
+  const std::vector<int32_t>& keys() const { return keys_; }
+  const std::vector<float>& values() const { return vals_; }
+  gw_topsim_stats_t stats() const { return stats_; }
+
+ private:
+  structures::Graph& g_;
+  int capacity, SAMPLE, STEP, variant_;
+  uint64_t seed_;
+  std::vector<int32_t> keys_, sizes_;
+  std::vector<float> vals_;
+  gw_topsim_stats_t stats_{};
+};
+struct TopSim_singleSample_M : TopSimM {  // TopSim_singleSample_M.java:33-54
+  TopSim_singleSample_M(structures::Graph& g, int M, int sample, uint64_t seed = 0, int step = 5)
+      : TopSimM(g, M, sample, GW_TOPSIM_SINGLE_SAMPLE, seed, step) {}
+};
+struct SingleRandomWalk_M : TopSimM {  // SingleRandomWalk_M.java:24-42
+  SingleRandomWalk_M(structures::Graph& g, int M, int sample, uint64_t seed = 0, int step = 5)
+      : TopSimM(g, M, sample, GW_TOPSIM_SINGLE_RW, seed, step) {}
+};
+
 // simrank.SimRank (SimRank.java:15-82): naive all-pairs SimRank on the GPU.
 class SimRank {
  public:
@@ -143,6 +175,8 @@ struct Print {
   static void printByOrder(const simrank::TopSimBase& sim, const std::string& outPath, int topk, int testTopK);
   static void printByOrder(const std::vector<double>& sim, int64_t V, const std::string& outPath, int topk,
                            int testTopK);
+  // Print.printByOrder(FixedCacheMap[] sim, outPath, topk) (Print.java:94-124)
+  static void printByOrder(const simrank::TopSimM& sim, const std::string& outPath, int topk);
   // Print.printByOrderAll (Print.java:55-84): same with "%.7f"
   static void printByOrderAll(const std::vector<double>& sim, int64_t V, const std::string& outPath, int topk,
                               int testTopK);

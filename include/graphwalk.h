@@ -226,6 +226,27 @@ int gw_topsim_host(gw_graph* g, int variant, int sample, int step, double C,
                    int topk, int32_t* out_ids, double* out_scores,
                    double* out_rows, int64_t* stats);
 
+/* ---- bounded-memory variants with FixedCacheMap (§8f-3) -------------------- */
+/* Replaces new TopSim_singleSample_M(g, M, sample).compute() (variant
+ * GW_TOPSIM_SINGLE_SAMPLE; TopSim_singleSample_M.java:33-239, the reference
+ * fixes STEP = 5) and new SingleRandomWalk_M(g, M, sample).compute()
+ * (GW_TOPSIM_SINGLE_RW; SingleRandomWalk_M.java:24-92): every pair update
+ * (float)(... / SAMPLE) is put() into a lxctools.FixedCacheMap(capacity =
+ * TOPK*M) in the reference's order (FixedCacheMap.java:32-50: add to a
+ * present key, insert while not full, else replace the minimum when larger).
+ * Per source r the map is then iterated (delMin, ascending) into
+ * out_keys_dev/out_vals_dev[r*capacity + i], i < out_size_dev[r] (-1 / 0
+ * padded).  Same Philox walks as gw_topsim.  capacity <= 4096.             */
+int gw_topsim_m(gw_graph* g, int variant, int capacity, int sample, int step,
+                double C, uint64_t seed, const int32_t* sources_dev, int64_t nsrc,
+                int32_t* out_keys_dev, float* out_vals_dev, int32_t* out_size_dev,
+                int64_t* stats_dev, void* stream);
+/* Host-buffer form (synchronous).                                           */
+int gw_topsim_m_host(gw_graph* g, int variant, int capacity, int sample,
+                     int step, double C, uint64_t seed, const int32_t* sources,
+                     int64_t nsrc, int32_t* out_keys, float* out_vals,
+                     int32_t* out_size, int64_t* stats);
+
 /* ---- naive SimRank (TopSim ground truth) ------------------------------------ */
 /* Replaces new SimRank(g).compute() + getResult() (SimRank.java:21-57, 79):
  * S := I; `iters` rounds (the reference's STEP = 3) of
@@ -258,6 +279,14 @@ int gw_write_sim_text_topk(const char* path, const int32_t* ids,
                            const double* scores, const int32_t* row_ids,
                            int64_t nrows, int topk, const char* sep,
                            int decimals);
+
+/* Print.printByOrder(FixedCacheMap[] sim, outPath, topk) (Print.java:94-124):
+ * per row the last `topk` entries of the ascending iteration, "%.6f" of the
+ * float values; rows as produced by gw_topsim_m.                            */
+int gw_write_sim_text_cachemap(const char* path, const int32_t* keys,
+                               const float* vals, const int32_t* sizes,
+                               const int32_t* row_ids, int64_t nrows,
+                               int capacity, int topk, const char* sep);
 
 #ifdef __cplusplus
 }

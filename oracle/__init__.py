@@ -51,6 +51,9 @@ def lib():
         L.or_walks_bitset.argtypes = [i64, v, v, v, d, d, u64, ci, i64, i64, ci, v, v, v, ci]
         L.or_topsim.argtypes = [i64, v, v, ci, ci, ci, d, u64, ci, i64, v, i64, v, v, ci]
         L.or_simrank_naive.argtypes = [i64, v, v, d, ci, v, ci]
+        L.or_topsim_m.argtypes = [i64, v, v, ci, ci, ci, d, u64, ci, v, i64, v, v, v, v, ci]
+        L.or_fcm_run.argtypes = [ci, i64, v, v, v, v]
+        L.or_fcm_run.restype = ci
         L.or_simrank_round_rows.argtypes = [i64, v, v, d, v, i64, i64, v, ci]
         L.or_simrank_round_rows.restype = i64
         _lib = L
@@ -183,6 +186,94 @@ def simrank_naive(offsets, nbrs, C, iters, nthreads=0):
     sim = np.zeros((n, n), np.float64)
     lib().or_simrank_naive(n, _p(off), _p(nb), float(C), int(iters), _p(sim), int(nthreads))
     return sim
+
+
+def topsim_m(offsets, nbrs, variant, sample, step, capacity, C=0.6, seed=0, sources=None, nthreads=0):
+    """TopSim_singleSample_M (variant 0) / SingleRandomWalk_M (variant 2) with
+    FixedCacheMap(capacity): per source the drained (ascending) keys/values
+    and sizes, plus stats."""
+    off = np.ascontiguousarray(offsets, np.int64)
+    nb = np.ascontiguousarray(nbrs, np.int32)
+    n = len(off) - 1
+    src = np.arange(n, dtype=np.int32) if sources is None else np.ascontiguousarray(sources, np.int32)
+    keys = np.full((len(src), capacity), -1, np.int32)
+    vals = np.zeros((len(src), capacity), np.float32)
+    size = np.zeros(len(src), np.int32)
+    st = np.zeros(4, np.int64)
+    lib().or_topsim_m(n, _p(off), _p(nb), int(variant), int(sample), int(step), float(C), int(seed),
+                      int(capacity), _p(src), len(src), _p(keys), _p(vals), _p(size), _p(st), int(nthreads))
+    return keys, vals, size, dict(extensions=int(st[0]), pair_updates=int(st[1]), max_frontier=int(st[2]),
+                                  walkers=int(st[3]))
+
+
+def fcm_run(nmax, keys, vals):
+    """FixedCacheMap(nmax): put (keys[i], vals[i]) in order, then iterate
+    (delMin, ascending) -> list of (key, value)."""
+    k = np.ascontiguousarray(keys, np.int32)
+    v = np.ascontiguousarray(vals, np.float32)
+    ok = np.zeros(nmax, np.int32)
+    ov = np.zeros(nmax, np.float32)
+    c = lib().or_fcm_run(int(nmax), len(k), _p(k), _p(v), _p(ok), _p(ov))
+    return [(int(ok[i]), float(ov[i])) for i in range(c)]
+
+
+class PyFixedCacheMap:
+    """Pure-Python literal FixedCacheMap (FixedCacheMap.java:14-127), float32
+    arithmetic via numpy; cross-checks the C restatement."""
+
+    def __init__(self, nmax):
+        self.NMAX, self.N = nmax, 0
+        self.keys = [0] * (nmax + 1)
+        self.values = [np.float32(0)] * (nmax + 1)
+        self.key2Index = {}
+
+    def put(self, key, value):
+        value = np.float32(value)
+        index = self.key2Index.get(key)
+        if index is not None:
+            self.values[index] = np.float32(self.values[index] + value)
+            self._sink(index)
+        elif self.N < self.NMAX:
+            self.N += 1
+            self.keys[self.N], self.values[self.N] = key, value
+            self.key2Index[key] = self.N
+            self._swim(self.N)
+        elif value > self.values[1]:
+            del self.key2Index[self.keys[1]]
+            self.keys[1], self.values[1] = key, value
+            self.key2Index[key] = 1
+            self._sink(1)
+
+    def _sink(self, i):
+        while 2 * i <= self.N:
+            j = 2 * i
+            if j < self.N and self.values[j] > self.values[j + 1]:
+                j += 1
+            if not self.values[i] > self.values[j]:
+                break
+            self._exch(i, j)
+            i = j
+
+    def _swim(self, i):
+        while i > 1 and self.values[i // 2] > self.values[i]:
+            self._exch(i, i // 2)
+            i //= 2
+
+    def _exch(self, a, b):
+        self.key2Index[self.keys[a]] = b
+        self.key2Index[self.keys[b]] = a
+        self.keys[a], self.keys[b] = self.keys[b], self.keys[a]
+        self.values[a], self.values[b] = self.values[b], self.values[a]
+
+    def drain(self):
+        out = []
+        while self.N > 0:
+            out.append((self.keys[1], float(self.values[1])))
+            self.key2Index.pop(self.keys[1], None)
+            self._exch(1, self.N)
+            self.N -= 1
+            self._sink(1)
+        return out
 
 
 def simrank_round_rows(offsets, nbrs, C, S, rb, re, nthreads=0):

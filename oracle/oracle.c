@@ -348,13 +348,135 @@ static int first_meet(const int32_t* path, int dst) { /* isFirstMeet(path, 0, ds
   return 1;
 }
 
+/* lxctools.FixedCacheMap (FixedCacheMap.java:14-110), literal: 1-based  */
+/* min-heap on float values, key2Index map, sink/swim/exch as in Java.     */
+typedef struct {
+  int NMAX, N;
+  int32_t* keys;
+  float* vals;
+  int32_t* hk; /* hash: key -> heap index (stands in for HashMap<Integer,Short>) */
+  int32_t* hv;
+  int hmask;
+} fcm;
+
+static void fcm_init(fcm* m, int nmax) {
+  m->NMAX = nmax;
+  m->N = 0;
+  m->keys = (int32_t*)calloc((size_t)nmax + 1, sizeof(int32_t));
+  m->vals = (float*)calloc((size_t)nmax + 1, sizeof(float));
+  int hs = 4;
+  while (hs < 4 * (nmax + 1)) hs <<= 1;
+  m->hmask = hs - 1;
+  m->hk = (int32_t*)malloc(sizeof(int32_t) * hs);
+  m->hv = (int32_t*)malloc(sizeof(int32_t) * hs);
+  for (int i = 0; i < hs; ++i) m->hk[i] = -1;
+}
+static void fcm_free(fcm* m) { free(m->keys); free(m->vals); free(m->hk); free(m->hv); }
+static void fcm_clear(fcm* m) {
+  m->N = 0;
+  for (int i = 0; i <= m->hmask; ++i) m->hk[i] = -1;
+}
+static uint32_t fcm_h(int32_t k) { return (uint32_t)k * 0x9E3779B1u; }
+static int fcm_get(const fcm* m, int32_t k) {
+  for (uint32_t h = fcm_h(k) & m->hmask;; h = (h + 1) & m->hmask) {
+    if (m->hk[h] == k) return m->hv[h];
+    if (m->hk[h] == -1) return -1;
+  }
+}
+static void fcm_hput(fcm* m, int32_t k, int v) {
+  uint32_t h = fcm_h(k) & m->hmask;
+  while (m->hk[h] != -1 && m->hk[h] != k) h = (h + 1) & m->hmask;
+  m->hk[h] = k;
+  m->hv[h] = v;
+}
+static void fcm_hdel(fcm* m, int32_t k) { /* linear probing, backward-shift delete */
+  uint32_t h = fcm_h(k) & m->hmask;
+  while (m->hk[h] != k) {
+    if (m->hk[h] == -1) return;
+    h = (h + 1) & m->hmask;
+  }
+  uint32_t i = h;
+  for (;;) {
+    m->hk[i] = -1;
+    uint32_t j = i;
+    for (;;) {
+      j = (j + 1) & m->hmask;
+      if (m->hk[j] == -1) return;
+      uint32_t home = fcm_h(m->hk[j]) & m->hmask;
+      /* move j back to i when home is not cyclically in (i, j] */
+      int in = (i <= j) ? (home > i && home <= j) : (home > i || home <= j);
+      if (!in) break;
+    }
+    m->hk[i] = m->hk[j];
+    m->hv[i] = m->hv[j];
+    i = j;
+  }
+}
+static void fcm_exch(fcm* m, int a, int b) { /* :86-98 */
+  fcm_hput(m, m->keys[a], b);
+  fcm_hput(m, m->keys[b], a);
+  int32_t tk = m->keys[a];
+  m->keys[a] = m->keys[b];
+  m->keys[b] = tk;
+  float tv = m->vals[a];
+  m->vals[a] = m->vals[b];
+  m->vals[b] = tv;
+}
+static void fcm_sink(fcm* m, int i) { /* :61-69 */
+  while (2 * i <= m->N) {
+    int j = 2 * i;
+    if (j < m->N && m->vals[j] > m->vals[j + 1]) j++;
+    if (!(m->vals[i] > m->vals[j])) break;
+    fcm_exch(m, i, j);
+    i = j;
+  }
+}
+static void fcm_swim(fcm* m, int i) { /* :73-78 */
+  while (i > 1 && m->vals[i / 2] > m->vals[i]) {
+    fcm_exch(m, i, i / 2);
+    i = i / 2;
+  }
+}
+static void fcm_put(fcm* m, int32_t key, float value) { /* :32-50 */
+  int idx = fcm_get(m, key);
+  if (idx >= 0) {
+    m->vals[idx] += value;
+    fcm_sink(m, idx);
+  } else if (m->N < m->NMAX) {
+    m->N++;
+    m->keys[m->N] = key;
+    m->vals[m->N] = value;
+    fcm_hput(m, key, m->N);
+    fcm_swim(m, m->N);
+  } else if (value > m->vals[1]) {
+    fcm_hdel(m, m->keys[1]);
+    m->keys[1] = key;
+    m->vals[1] = value;
+    fcm_hput(m, key, 1);
+    fcm_sink(m, 1);
+  }
+}
+/* iteration = repeated delMin (:104-127): ascending order, empties the map */
+static int fcm_drain(fcm* m, int32_t* ok, float* ov) {
+  int c = 0;
+  while (m->N > 0) {
+    ok[c] = m->keys[1];
+    ov[c] = m->vals[1];
+    c++;
+    fcm_hdel(m, m->keys[1]);
+    fcm_exch(m, 1, m->N--);
+    fcm_sink(m, 1);
+  }
+  return c;
+}
+
 typedef struct {
   int64_t ext, upd, maxf, walkers;
 } tstats;
 
 static void topsim_one(const int64_t* off, const int32_t* nbrs, int variant, int SAMPLE, int STEP,
                        const double* cache, uint32_t k0, uint32_t k1, int rng, jrand* jr, int32_t src,
-                       double* row, pqueue* A, pqueue* B, tstats* st) {
+                       double* row, pqueue* A, pqueue* B, tstats* st, fcm* map) {
   const int L = 2 * STEP;
   if (variant == 2) { /* SingleRandomWalk.walk :53-72 + computePathSim :81-92 */
     int32_t* path = (int32_t*)malloc(sizeof(int32_t) * (L + 1));
@@ -384,7 +506,11 @@ static void topsim_one(const int64_t* off, const int32_t* nbrs, int variant, int
         if (target == src) continue;
         if (first_meet(path, 2 * ii)) {
           double dm = (double)(off[inter + 1] - off[inter]), dt = (double)(off[target + 1] - off[target]);
-          row[target] += ((cache[ii] * dm) / dt) / (double)SAMPLE;
+          double incre = ((cache[ii] * dm) / dt) / (double)SAMPLE;
+          if (map)
+            fcm_put(map, target, (float)incre); /* SingleRandomWalk_M.java:computePathSim */
+          else
+            row[target] += incre;
           st->upd++;
         }
       }
@@ -420,7 +546,10 @@ static void topsim_one(const int64_t* off, const int32_t* nbrs, int variant, int
             if (first_meet(path, 2 * i)) {
               double dm = (double)(off[inter + 1] - off[inter]);
               double dt = (double)(off[target + 1] - off[target]);
-              row[target] += ((mass[2 * i] * cache[i]) * dm) / dt; /* :189 */
+              if (map) /* TopSim_singleSample_M.java:224-225 */
+                fcm_put(map, target, (float)((((mass[2 * i] * cache[i]) * dm) / dt) / (double)SAMPLE));
+              else
+                row[target] += ((mass[2 * i] * cache[i]) * dm) / dt; /* :189 */
               st->upd++;
             }
           }
@@ -482,7 +611,7 @@ static void topsim_one(const int64_t* off, const int32_t* nbrs, int variant, int
     *B = tmp;
     pathLen++;
   }
-  row[src] = 0.0; /* sim[i][i] = 0 (:52) */
+  if (row) row[src] = 0.0; /* sim[i][i] = 0 (:52) */
 }
 
 /* rows[r*n + t] = sim[sources[r]][t]; stats: ext, upd, maxf, walkers */
@@ -501,7 +630,7 @@ void or_topsim(int64_t n, const int64_t* off, const int32_t* nbrs, int variant, 
     pqueue A = {0}, B = {0};
     tstats st = {0, 0, 0, 0};
     for (int64_t r = 0; r < nsrc; ++r)
-      topsim_one(off, nbrs, variant, sample, step, cache, k0, k1, 1, &jr, sources[r], rows + r * n, &A, &B, &st);
+      topsim_one(off, nbrs, variant, sample, step, cache, k0, k1, 1, &jr, sources[r], rows + r * n, &A, &B, &st, NULL);
     e = st.ext;
     u = st.upd;
     mf = st.maxf;
@@ -520,7 +649,7 @@ void or_topsim(int64_t n, const int64_t* off, const int32_t* nbrs, int variant, 
 #pragma omp for schedule(dynamic, 1)
 #endif
       for (int64_t r = 0; r < nsrc; ++r)
-        topsim_one(off, nbrs, variant, sample, step, cache, k0, k1, 0, NULL, sources[r], rows + r * n, &A, &B, &st);
+        topsim_one(off, nbrs, variant, sample, step, cache, k0, k1, 0, NULL, sources[r], rows + r * n, &A, &B, &st, NULL);
       e += st.ext;
       u += st.upd;
       w += st.walkers;
@@ -535,6 +664,64 @@ void or_topsim(int64_t n, const int64_t* off, const int32_t* nbrs, int variant, 
     stats[2] = mf;
     stats[3] = w;
   }
+}
+
+/* TopSim_singleSample_M (variant 0) / SingleRandomWalk_M (variant 2): the  */
+/* same walks as or_topsim (Philox keys), every pair update put() into a    */
+/* FixedCacheMap(capacity) in the reference's order; per source the map is   */
+/* drained ascending (its iteration order): out_keys/out_vals[r*cap + i],   */
+/* out_size[r].                                                            */
+void or_topsim_m(int64_t n, const int64_t* off, const int32_t* nbrs, int variant, int sample, int step,
+                 double C, uint64_t seed, int capacity, const int32_t* sources, int64_t nsrc, int32_t* out_keys,
+                 float* out_vals, int32_t* out_size, int64_t* stats, int nthreads) {
+  (void)n;
+  double cache[32];
+  for (int i = 0; i < 32; ++i) cache[i] = 0.0;
+  for (int i = 1; i <= step && i < 32; ++i) cache[i] = pow(C, (double)i);
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32) ^ GW_TAG_TOPSIM;
+  int64_t e = 0, u = 0, mf = 0, w = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel reduction(+ : e, u, w) reduction(max : mf)
+#endif
+  {
+    pqueue A = {0}, B = {0};
+    tstats st = {0, 0, 0, 0};
+    fcm m;
+    fcm_init(&m, capacity);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+    for (int64_t r = 0; r < nsrc; ++r) {
+      fcm_clear(&m);
+      topsim_one(off, nbrs, variant, sample, step, cache, k0, k1, 0, NULL, sources[r], NULL, &A, &B, &st, &m);
+      out_size[r] = fcm_drain(&m, out_keys + r * (int64_t)capacity, out_vals + r * (int64_t)capacity);
+    }
+    e += st.ext;
+    u += st.upd;
+    w += st.walkers;
+    if (st.maxf > mf) mf = st.maxf;
+    fcm_free(&m);
+    free(A.cur); free(A.mass); free(A.walker);
+    free(B.cur); free(B.mass); free(B.walker);
+  }
+  if (stats) {
+    stats[0] = e;
+    stats[1] = u;
+    stats[2] = mf;
+    stats[3] = w;
+  }
+}
+
+/* FixedCacheMap.main (FixedCacheMap.java:134-148) as a known-answer check:  */
+/* puts (key, value) in order into a map of capacity nmax, drains ascending. */
+int or_fcm_run(int nmax, int64_t nput, const int32_t* keys, const float* vals, int32_t* ok, float* ov) {
+  fcm m;
+  fcm_init(&m, nmax);
+  for (int64_t i = 0; i < nput; ++i) fcm_put(&m, keys[i], vals[i]);
+  int c = fcm_drain(&m, ok, ov);
+  fcm_free(&m);
+  return c;
 }
 
 /* ------------------------------------------------------------------------ */

@@ -242,3 +242,44 @@ def test_bitset_walks_match_second_order_distribution(oracle, p, q):
         sd = np.sqrt(pr * (1 - pr) / tot)
         worst = max(worst, float(np.max(np.abs(emp - pr) / np.maximum(sd, 1e-12))))
     assert worst < 5.5, worst
+
+
+def test_fixed_cache_map_reference_main(oracle):
+    """FixedCacheMap.main (FixedCacheMap.java:134-148): the reference's own
+    example, capacity 3 -> drains (1, 1.1f), (2, 3f), (4, 16f)."""
+    got = oracle.fcm_run(3, [1, 2, 3, 4, 4, 1, 5], [0.5, 3, 0.1, 8, 8, 0.6, 1])
+    assert [k for k, _ in got] == [1, 2, 4]
+    assert np.array_equal(np.float32([v for _, v in got]), np.float32([1.1, 3.0, 16.0]))
+    py = oracle.PyFixedCacheMap(3)
+    for k, v in zip([1, 2, 3, 4, 4, 1, 5], [0.5, 3, 0.1, 8, 8, 0.6, 1]):
+        py.put(k, v)
+    assert py.drain() == got
+
+
+@pytest.mark.parametrize("nmax,nkeys,nput", [(5, 40, 400), (16, 30, 2000), (64, 1000, 5000), (200, 150, 3000)])
+def test_fixed_cache_map_c_equals_python(oracle, nmax, nkeys, nput):
+    """C restatement == literal Python port on random put streams (eviction,
+    re-insertion of evicted keys, float accumulation, ties)."""
+    rng = np.random.default_rng(nmax)
+    keys = rng.integers(0, nkeys, nput).astype(np.int32)
+    vals = (np.round(rng.random(nput) * 16) / 16 * rng.choice([1e-3, 1.0], nput)).astype(np.float32)
+    got = oracle.fcm_run(nmax, keys, vals)
+    py = oracle.PyFixedCacheMap(nmax)
+    for k, v in zip(keys.tolist(), vals.tolist()):
+        py.put(k, v)
+    assert py.drain() == got
+
+
+def test_topsim_m_oracle_no_eviction_matches_topsim(oracle):
+    """TopSim_singleSample_M with a capacity that never evicts == float
+    accumulation of TopSim_singleSample's updates / SAMPLE (same Philox walks)."""
+    offs, nbrs = _java_graph_csr(os.path.join(DATA, "moreno_crime_crime.txt"), 1380, "\t")
+    src = np.arange(0, 1380, 97, dtype=np.int32)
+    keys, vals, size, st = oracle.topsim_m(offs, nbrs, 0, 300, 3, 4096, C=0.6, seed=5, sources=src, nthreads=8)
+    rows, st2 = oracle.topsim(offs, nbrs, 0, 300, 3, C=0.6, seed=5, sources=src, nthreads=8)
+    assert st["pair_updates"] == st2["pair_updates"] and st["extensions"] == st2["extensions"]
+    for r in range(len(src)):
+        ks = keys[r, :size[r]]
+        assert set(ks.tolist()) == set(np.nonzero(rows[r])[0].tolist())
+        np.testing.assert_allclose(vals[r, :size[r]], rows[r][ks] / 300, rtol=1e-5)
+        assert np.all(np.diff(vals[r, :size[r]]) >= 0)  # ascending iteration
