@@ -21,7 +21,7 @@ OUT = os.path.join(HERE, "gwamd", "libgraphwalk.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("GW_OFFLOAD_ARCH", "gfx950")
 
-HIP_SRCS = ["gw_n2v.hip", "gw_n2v_bitset.hip", "gw_topsim.hip", "gw_simrank.hip", "gw_topsim_m.hip"]
+HIP_SRCS = ["gw_n2v.hip", "gw_n2v_bitset.hip", "gw_topsim.hip", "gw_simrank.hip", "gw_topsim_m.hip", "gw_topsim_d.hip"]
 CXX_SRCS = ["gw_graph_host.cpp", "gw_capi.cpp"]
 HEADERS = ["gw_internal.h", "gw_philox.h", "gw_device_common.h"]
 

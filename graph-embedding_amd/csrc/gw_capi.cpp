@@ -27,6 +27,8 @@ int gw_write_sim_topk_impl(const char* path, const int32_t* ids, const double* s
 int gw_write_sim_cachemap_impl(const char* path, const int32_t* keys, const float* vals, const int32_t* sizes,
                                const int32_t* row_ids, int64_t nrows, int capacity, int topk,
                                const std::string& sep, std::string* err);
+void gw_select_fixed_max_pq_impl(const double* rows, int64_t nrows, int64_t n, int k, double min_score,
+                                 int32_t* out_ids);
 int gw_hip_device_count(int* count);
 
 static thread_local std::string tls_err;
@@ -340,6 +342,25 @@ int gw_topsim_m(gw_graph* g, int variant, int capacity, int sample, int step, do
                                 out_vals_dev, out_size_dev, stats_dev, stream));
 }
 
+int gw_topsim_double(gw_graph* g, int sample, int step, double C, uint64_t seed, double* sim_dev, void* stream) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  if (g->n > 0 && !sim_dev) return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
+  return ret(g, gw_dev_topsim_double(g, sample, step, C, seed, sim_dev, stream));
+}
+
+int gw_topsim_dev(gw_graph* g, int sample, int step, int topK, int singleStep, double C, uint64_t seed,
+                  const int32_t* cand_dev, double* sim_dev, void* stream) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  if (g->n > 0 && (!sim_dev || (topK > 0 && !cand_dev))) return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
+  return ret(g, gw_dev_topsim_dev(g, sample, step, topK, singleStep, C, seed, cand_dev, sim_dev, stream));
+}
+
+int gw_double_random_walk(gw_graph* g, int sample, int step, double C, uint64_t seed, double* sim_dev, void* stream) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  if (g->n > 0 && !sim_dev) return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
+  return ret(g, gw_dev_double_random_walk(g, sample, step, C, seed, sim_dev, stream));
+}
+
 int gw_simrank_naive(gw_graph* g, double C, int iters, double* sim_dev, void* stream) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
   if (g->device < 0) return ret(g, gw_fail(g, GW_ERR_STATE, "graph is not on a device"));
@@ -378,6 +399,12 @@ int gw_write_sim_text_topk(const char* path, const int32_t* ids, const double* s
   std::string err;
   int rc = gw_write_sim_topk_impl(path, ids, scores, row_ids, nrows, topk, sep ? sep : ",", decimals, &err);
   if (rc != GW_OK) return gw_fail(nullptr, rc, "%s", err.c_str());
+  return GW_OK;
+}
+
+int gw_select_fixed_max_pq(const double* rows, int64_t nrows, int64_t n, int k, double min_score, int32_t* out_ids) {
+  if ((nrows > 0 && (!rows || !out_ids)) || n < 0 || k < 0) return gw_fail(nullptr, GW_ERR_INVALID, "bad arguments");
+  gw_select_fixed_max_pq_impl(rows, nrows, n, k, min_score, out_ids);
   return GW_OK;
 }
 

@@ -775,3 +775,31 @@ int gw_write_sim_cachemap_impl(const char* path, const int32_t* keys, const floa
   if (rc != GW_OK) *err = "write failed";
   return rc;
 }
+
+// TopSim_Dev.compute (TopSim_Dev.java:64-71): FixedMaxPQ(k) offered every
+// (j, rows[i][j]) with rows[i][j] >= min_score in j order, then
+// sortedElement(); out_ids[i*k + r] (-1 padded).
+void gw_select_fixed_max_pq_impl(const double* rows, int64_t nrows, int64_t n, int k, double min_score,
+                                 int32_t* out_ids) {
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int64_t r = 0; r < nrows; ++r) {
+    const double* row = rows + r * n;
+    JavaPQ pq;
+    pq.q.reserve(k + 1);
+    for (int64_t i = 0; i < n; ++i) {
+      if (!(row[i] >= min_score)) continue;
+      JPair e{(int32_t)i, row[i]};
+      if ((int64_t)pq.q.size() < k) {
+        pq.offer(e);
+      } else if (k > 0 && JavaPQ::cmp(pq.q[0], e) < 0) {
+        pq.poll();
+        pq.offer(e);
+      }
+    }
+    std::vector<JPair> sorted(pq.q);
+    std::stable_sort(sorted.begin(), sorted.end(), [](const JPair& a, const JPair& b) {
+      return JavaPQ::cmp(a, b) > 0;
+    });
+    for (int q = 0; q < k; ++q) out_ids[r * (int64_t)k + q] = q < (int)sorted.size() ? sorted[(size_t)q].key : -1;
+  }
+}

@@ -135,6 +135,11 @@ int gw_dev_n2v_walks_replay(gw_graph* g, int walk_len, int64_t nwalks,
                             int32_t* out_len, int64_t* uniforms_used);
 void gw_dev_bitset_release(gw_graph* g);
 void gw_dev_simrank_release(gw_graph* g);
+int gw_dev_topsim_double(gw_graph* g, int sample, int step, double C, uint64_t seed, double* sim_dev, void* stream);
+int gw_dev_topsim_dev(gw_graph* g, int sample_total, int step, int topK, int singleStep, double C, uint64_t seed,
+                      const int32_t* cand_dev, double* sim_dev, void* stream);
+int gw_dev_double_random_walk(gw_graph* g, int sample, int step, double C, uint64_t seed, double* sim_dev,
+                              void* stream);
 int gw_dev_topsim_m(gw_graph* g, int variant, int capacity, int sample, int step, double C, uint64_t seed,
                     const int32_t* sources_dev, int64_t nsrc, int32_t* out_keys_dev, float* out_vals_dev,
                     int32_t* out_size_dev, int64_t* stats_dev, void* stream);

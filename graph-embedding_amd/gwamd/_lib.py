@@ -40,6 +40,9 @@ N2V_BITSET = 2
 TOPSIM_SINGLE_SAMPLE = 0
 TOPSIM_ENUMERATE = 1
 TOPSIM_SINGLE_RW = 2
+DOUBLE_SAMPLE = 0
+DOUBLE_DEV = 1
+DOUBLE_RANDOM_WALK = 2
 
 
 class GraphWalkError(RuntimeError):
@@ -114,6 +117,12 @@ SIGNATURES = {
                                    P, P, P, P, P]),
     "gw_topsim_m_host": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, U64, P,
                                         I64, P, P, P, P]),
+    "gw_topsim_double": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, D, U64, P, P]),
+    "gw_topsim_dev": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, U64, P, P, P]),
+    "gw_double_random_walk": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, D, U64, P, P]),
+    "gw_double_sim_host": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          D, U64, P, P]),
+    "gw_select_fixed_max_pq": (ctypes.c_int, [P, I64, I64, ctypes.c_int, D, P]),
     "gw_simrank_naive": (ctypes.c_int, [P, D, ctypes.c_int, P, P]),
     "gw_simrank_naive_host": (ctypes.c_int, [P, D, ctypes.c_int, P]),
     "gw_write_walks_text": (ctypes.c_int, [P, CP, P, P, I64, ctypes.c_int]),

@@ -242,6 +242,84 @@ class SingleRandomWalk_M(_TopSimM):
     VARIANT = C.TOPSIM_SINGLE_RW
 
 
+class _DoubleBase:
+    def __init__(self, g, C_=C_DEFAULT, seed=0):
+        self.g = g
+        self.COUNT = g.getVCount()
+        self.C = float(C_)
+        self.seed = int(seed)
+        self._sim = None
+
+    def _dense(self, fn, *args):
+        import torch
+        g = self.g
+        g._ensure_device()
+        dev = torch.device("cuda", g.device)
+        sim = torch.empty((self.COUNT, self.COUNT), dtype=torch.float64, device=dev)
+        h = g._g.handle
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        C.check(fn(h, *args, C.ptr(sim), stream), h)
+        self._sim = sim.cpu().numpy()
+
+    def getResult(self):
+        if self._sim is None:
+            raise RuntimeError("call compute() first")
+        return self._sim
+
+
+class TopSim_doubleSample(_DoubleBase):
+    """simrank.TopSim_doubleSample (TopSim_doubleSample.java:20-197)."""
+
+    def __init__(self, g, sample, step, C_=C_DEFAULT, seed=0):
+        super().__init__(g, C_, seed)
+        self.SAMPLE, self.STEP = int(sample), int(step)
+
+    def compute(self):
+        self._dense(C.lib().gw_topsim_double, self.SAMPLE, self.STEP, self.C, self.seed)
+
+
+class DoubleRandomWalk(_DoubleBase):
+    """simrank.DoubleRandomWalk (DoubleRandomWalk.java:15-95)."""
+
+    def __init__(self, g, sample, step, C_=C_DEFAULT, seed=0):
+        super().__init__(g, C_, seed)
+        self.SAMPLE, self.STEP = int(sample), int(step)
+
+    def compute(self):
+        self._dense(C.lib().gw_double_random_walk, self.SAMPLE, self.STEP, self.C, self.seed)
+
+
+def select_candidates(candidate, k, min_score=MIN):
+    """TopSim_Dev's candidate choice (TopSim_Dev.java:64-71): FixedMaxPQ(k)
+    over candidate[i][j] >= MIN, sortedElement() order -> int32 [n, k], -1 padded."""
+    cand = np.ascontiguousarray(candidate, np.float64)
+    out = np.full((cand.shape[0], int(k)), -1, np.int32)
+    C.check(C.lib().gw_select_fixed_max_pq(C.ptr(cand), cand.shape[0], cand.shape[1], int(k), float(min_score),
+                                           C.ptr(out)))
+    return out
+
+
+class TopSim_Dev(_DoubleBase):
+    """simrank.TopSim_Dev (TopSim_Dev.java:24-101): candidate refinement."""
+
+    def __init__(self, g, sample, step, topK, singleStep, C_=C_DEFAULT, seed=0):
+        super().__init__(g, C_, seed)
+        self.sample_total, self.STEP = int(sample), int(step)
+        self.singleK, self.singleStep = int(topK), int(singleStep)
+        # SAMPLE = (int)(((step-singleStep)*sample*2.0)/((double)step*(topK+1.0))) (:33)
+        self.SAMPLE = int(((step - singleStep) * sample * 2.0) / (float(step) * (topK + 1.0)))
+
+    def compute(self, candidate):
+        import torch
+        cand = candidate if (isinstance(candidate, np.ndarray) and candidate.dtype == np.int32
+                             and candidate.ndim == 2 and candidate.shape[1] == self.singleK) \
+            else select_candidates(candidate, self.singleK)
+        dev = torch.device("cuda", self.g.device)
+        cd = torch.as_tensor(np.ascontiguousarray(cand, np.int32), device=dev)
+        self._dense(C.lib().gw_topsim_dev, self.sample_total, self.STEP, self.singleK, self.singleStep, self.C,
+                    self.seed, C.ptr(cd))
+
+
 class SimRank:
     """simrank.SimRank (SimRank.java:15-82): naive SimRank, STEP = 3 rounds
     (the reference's private field; `step` overrides it), C from

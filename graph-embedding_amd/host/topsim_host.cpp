@@ -116,6 +116,21 @@ void TopSimM::compute() {
   stats_.walkers = st[3];
 }
 
+void DoubleWalkBase::run(int kind, int sample, int step, int topK, int singleStep, const int32_t* cand) {
+  const int64_t V = g_.getVCount();
+  sim_.assign((size_t)(V * V), 0.0);
+  gw::check(gw_double_sim_host(g_.handle(), kind, sample, step, topK, singleStep, conf::MyConfiguration::C, seed_,
+                               cand, sim_.data()),
+            g_.handle());
+}
+
+void TopSim_Dev::compute(const std::vector<double>& candidate) {
+  const int64_t V = g_.getVCount();
+  std::vector<int32_t> cand((size_t)(V * singleK), -1);
+  gw::check(gw_select_fixed_max_pq(candidate.data(), V, V, singleK, conf::MyConfiguration::MIN, cand.data()));
+  run(GW_DOUBLE_DEV, sample_, STEP, singleK, singleStep_, cand.data());
+}
+
 void SimRank::compute() {
   const int64_t V = g_.getVCount();
   sim_.assign((size_t)(V * V), 0.0);

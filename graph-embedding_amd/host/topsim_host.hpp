@@ -153,6 +153,50 @@ struct SingleRandomWalk_M : TopSimM {  // SingleRandomWalk_M.java:24-42
       : TopSimM(g, M, sample, GW_TOPSIM_SINGLE_RW, seed, step) {}
 };
 
+// Double-walk variants (§8f-4): dense V*V results, row-major.
+class DoubleWalkBase {
+ public:
+  const std::vector<double>& getResult() const { return sim_; }
+  int getVCount() const { return g_.getVCount(); }
+
+ protected:
+  DoubleWalkBase(structures::Graph& g, uint64_t seed) : g_(g), seed_(seed) {}
+  void run(int kind, int sample, int step, int topK, int singleStep, const int32_t* cand);
+  structures::Graph& g_;
+  uint64_t seed_;
+  std::vector<double> sim_;
+};
+// simrank.TopSim_doubleSample (TopSim_doubleSample.java:30-197)
+class TopSim_doubleSample : public DoubleWalkBase {
+ public:
+  TopSim_doubleSample(structures::Graph& g, int sample, int step, uint64_t seed = 0)
+      : DoubleWalkBase(g, seed), SAMPLE(sample), STEP(step) {}
+  void compute() { run(GW_DOUBLE_SAMPLE, SAMPLE, STEP, 0, 0, nullptr); }
+
+ private:
+  int SAMPLE, STEP;
+};
+// simrank.DoubleRandomWalk (DoubleRandomWalk.java:25-95)
+class DoubleRandomWalk : public DoubleWalkBase {
+ public:
+  DoubleRandomWalk(structures::Graph& g, int sample, int step, uint64_t seed = 0)
+      : DoubleWalkBase(g, seed), SAMPLE(sample), STEP(step) {}
+  void compute() { run(GW_DOUBLE_RANDOM_WALK, SAMPLE, STEP, 0, 0, nullptr); }
+
+ private:
+  int SAMPLE, STEP;
+};
+// simrank.TopSim_Dev (TopSim_Dev.java:31-95): compute(candidate V*V)
+class TopSim_Dev : public DoubleWalkBase {
+ public:
+  TopSim_Dev(structures::Graph& g, int sample, int step, int topK, int singleStep, uint64_t seed = 0)
+      : DoubleWalkBase(g, seed), sample_(sample), STEP(step), singleK(topK), singleStep_(singleStep) {}
+  void compute(const std::vector<double>& candidate);
+
+ private:
+  int sample_, STEP, singleK, singleStep_;
+};
+
 // simrank.SimRank (SimRank.java:15-82): naive all-pairs SimRank on the GPU.
 class SimRank {
  public:

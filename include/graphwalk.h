@@ -247,6 +247,43 @@ int gw_topsim_m_host(gw_graph* g, int variant, int capacity, int sample,
                      int64_t nsrc, int32_t* out_keys, float* out_vals,
                      int32_t* out_size, int64_t* stats);
 
+/* ---- double-walk variants (§8f-4) ------------------------------------------ */
+/* kinds for gw_double_sim_host                                              */
+#define GW_DOUBLE_SAMPLE 0      /* TopSim_doubleSample */
+#define GW_DOUBLE_DEV 1         /* TopSim_Dev          */
+#define GW_DOUBLE_RANDOM_WALK 2 /* DoubleRandomWalk    */
+/* Replaces new TopSim_doubleSample(g, sample, step).compute() + getResult()
+ * (TopSim_doubleSample.java:30-197): per vertex the TopSim BFS over `step`
+ * levels, paths[src][target][s] = mass of the LAST queued path reaching
+ * target at level s; sim[i][j] = sum_x sum_s C^s P[i][x][s] P[j][x][s]
+ * (i < j, mirrored, diag 0).  sim_dev[n*n]; Philox keys as gw_topsim.       */
+int gw_topsim_double(gw_graph* g, int sample, int step, double C,
+                     uint64_t seed, double* sim_dev, void* stream);
+/* Replaces new TopSim_Dev(g, sample, step, topK, singleStep).compute(cand)
+ * (TopSim_Dev.java:31-95): SAMPLE = (int)((step-singleStep)*sample*2 /
+ * (step*(topK+1))); for every i its candidates cand_dev[i*topK + r] (as
+ * gw_select_fixed_max_pq gives them, -1 padded) are each freshly sampled
+ * (Philox call 1 + i*topK + r) and sim[i][j] = getSim; other entries 0.    */
+int gw_topsim_dev(gw_graph* g, int sample, int step, int topK, int singleStep,
+                  double C, uint64_t seed, const int32_t* cand_dev,
+                  double* sim_dev, void* stream);
+/* Replaces new DoubleRandomWalk(g, sample, step).compute()
+ * (DoubleRandomWalk.java:25-91): `sample` uniform walks of `step` steps per
+ * vertex, sim[v][w] = sum over walk pairs of C^(t+1) at their first meeting
+ * step t, / sample^2 (v < w, mirrored, diag 0).                            */
+int gw_double_random_walk(gw_graph* g, int sample, int step, double C,
+                          uint64_t seed, double* sim_dev, void* stream);
+/* Host-buffer form of the three (kind = GW_DOUBLE_*): sim[n*n] on the host,
+ * cand[n*topK] on the host for GW_DOUBLE_DEV (ignored otherwise).           */
+int gw_double_sim_host(gw_graph* g, int kind, int sample, int step, int topK,
+                       int singleStep, double C, uint64_t seed,
+                       const int32_t* cand, double* sim);
+/* TopSim_Dev's candidate choice (TopSim_Dev.java:64-71): per row a
+ * FixedMaxPQ(k) offered every (j, rows[r][j] >= min_score) in j order, then
+ * sortedElement() -> out_ids[r*k + i] (-1 padded).  Host code.             */
+int gw_select_fixed_max_pq(const double* rows, int64_t nrows, int64_t n, int k,
+                           double min_score, int32_t* out_ids);
+
 /* ---- naive SimRank (TopSim ground truth) ------------------------------------ */
 /* Replaces new SimRank(g).compute() + getResult() (SimRank.java:21-57, 79):
  * S := I; `iters` rounds (the reference's STEP = 3) of

@@ -53,6 +53,10 @@ def lib():
         L.or_simrank_naive.argtypes = [i64, v, v, d, ci, v, ci]
         L.or_topsim_m.argtypes = [i64, v, v, ci, ci, ci, d, u64, ci, v, i64, v, v, v, v, ci]
         L.or_fcm_run.argtypes = [ci, i64, v, v, v, v]
+        L.or_topsim_levels.argtypes = [i64, v, v, ci, ci, u64, v, v, i64, v, ci]
+        L.or_topsim_double_sims.argtypes = [i64, v, ci, d, v, ci]
+        L.or_topsim_dev.argtypes = [i64, v, v, ci, ci, d, u64, v, ci, v, ci]
+        L.or_double_random_walk.argtypes = [i64, v, v, ci, ci, d, u64, v, ci]
         L.or_fcm_run.restype = ci
         L.or_simrank_round_rows.argtypes = [i64, v, v, d, v, i64, i64, v, ci]
         L.or_simrank_round_rows.restype = i64
@@ -206,6 +210,53 @@ def topsim_m(offsets, nbrs, variant, sample, step, capacity, C=0.6, seed=0, sour
                                   walkers=int(st[3]))
 
 
+def topsim_levels(offsets, nbrs, sample, step, tasks_v, tasks_call=None, seed=0, nthreads=0):
+    """TopSim_doubleSample/TopSim_Dev sample(): per task the last-wins mass
+    rows M[task, s-1, x] (0 = absent)."""
+    off = np.ascontiguousarray(offsets, np.int64)
+    nb = np.ascontiguousarray(nbrs, np.int32)
+    n = len(off) - 1
+    tv = np.ascontiguousarray(tasks_v, np.int32)
+    tc = np.zeros_like(tv) if tasks_call is None else np.ascontiguousarray(tasks_call, np.int32)
+    out = np.zeros((len(tv), step, n), np.float64)
+    lib().or_topsim_levels(n, _p(off), _p(nb), int(sample), int(step), int(seed), _p(tv), _p(tc), len(tv),
+                           _p(out), int(nthreads))
+    return out
+
+
+def topsim_double_sample(offsets, nbrs, sample, step, C=0.6, seed=0, nthreads=0):
+    """TopSim_doubleSample(g, sample, step).compute() -> dense sim."""
+    n = len(offsets) - 1
+    M = topsim_levels(offsets, nbrs, sample, step, np.arange(n, dtype=np.int32), seed=seed, nthreads=nthreads)
+    sim = np.zeros((n, n), np.float64)
+    lib().or_topsim_double_sims(n, _p(M), int(step), float(C), _p(sim), int(nthreads))
+    return sim
+
+
+def topsim_dev(offsets, nbrs, sample, step, cand, C=0.6, seed=0, nthreads=0):
+    """TopSim_Dev.compute(candidate) with candidate lists cand[n, K] (-1 pad);
+    `sample` is TopSim_Dev's derived SAMPLE."""
+    off = np.ascontiguousarray(offsets, np.int64)
+    nb = np.ascontiguousarray(nbrs, np.int32)
+    n = len(off) - 1
+    cd = np.ascontiguousarray(cand, np.int32)
+    sim = np.zeros((n, n), np.float64)
+    lib().or_topsim_dev(n, _p(off), _p(nb), int(sample), int(step), float(C), int(seed), _p(cd), cd.shape[1],
+                        _p(sim), int(nthreads))
+    return sim
+
+
+def double_random_walk(offsets, nbrs, sample, step, C=0.6, seed=0, nthreads=0):
+    """DoubleRandomWalk(g, sample, step).compute() -> dense sim."""
+    off = np.ascontiguousarray(offsets, np.int64)
+    nb = np.ascontiguousarray(nbrs, np.int32)
+    n = len(off) - 1
+    sim = np.zeros((n, n), np.float64)
+    lib().or_double_random_walk(n, _p(off), _p(nb), int(sample), int(step), float(C), int(seed), _p(sim),
+                                int(nthreads))
+    return sim
+
+
 def fcm_run(nmax, keys, vals):
     """FixedCacheMap(nmax): put (keys[i], vals[i]) in order, then iterate
     (delMin, ascending) -> list of (key, value)."""
@@ -354,8 +405,9 @@ def java_format_fixed(v, decimals=6):
     return format(d.quantize(q, rounding=decimal.ROUND_HALF_UP), "f")
 
 
-def java_fixed_max_pq_row(row, topk):
-    """FixedMaxPQ.offer over (i, row[i]) for i in order, then sortedElement()
+def java_fixed_max_pq_row(row, topk, min_score=None):
+    """FixedMaxPQ.offer over (i, row[i]) for i in order (only row[i] >=
+    min_score when given, as TopSim_Dev.java:66-68), then sortedElement()
     (FixedMaxPQ.java:30-39,72-76; java.util.PriorityQueue siftUp/siftDown;
     Collections.sort(reverseOrder()) is stable)."""
     q = []
@@ -389,6 +441,8 @@ def java_fixed_max_pq_row(row, topk):
         q[k] = x
 
     for i, val in enumerate(row):
+        if min_score is not None and not float(val) >= min_score:
+            continue
         e = (i, float(val))
         if len(q) < topk:
             q.append(None)

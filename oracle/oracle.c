@@ -713,6 +713,202 @@ void or_topsim_m(int64_t n, const int64_t* off, const int32_t* nbrs, int variant
   }
 }
 
+/* TopSim_doubleSample.sample / TopSim_Dev.sample (TopSim_doubleSample.java */
+/* :71-140, computePath :141-164): the BFS queue over STEP levels; at level  */
+/* s every queued path with target path[s] != source assigns               */
+/* paths[source][target][s] = path[s].sample in queue order (last wins).     */
+/* Task t = (vertex tv[t], Philox call tc[t]); out[t][s-1][x], 0 = absent.  */
+void or_topsim_levels(int64_t n, const int64_t* off, const int32_t* nbrs, int sample, int step, uint64_t seed,
+                      const int32_t* tv, const int32_t* tc, int64_t ntask, double* out, int nthreads) {
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32) ^ GW_TAG_TOPSIM;
+  const int L = step;
+  memset(out, 0, sizeof(double) * ntask * step * n);
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+#endif
+  {
+    pqueue A = {0}, B = {0};
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+    for (int64_t t = 0; t < ntask; ++t) {
+      const int32_t src = tv[t];
+      const uint32_t call = (uint32_t)tc[t];
+      double* row = out + t * step * n;
+      A.size = 0;
+      pq_reserve(&A, 1, L);
+      for (int q = 0; q <= L; ++q) {
+        A.cur[q] = -1;
+        A.mass[q] = 0.0;
+      }
+      A.cur[0] = src;
+      A.mass[0] = (double)sample;
+      A.walker[0] = -1;
+      A.size = 1;
+      int64_t next_walker = 0;
+      for (int pathLen = 0;; ++pathLen) {
+        if (pathLen >= 1) { /* computePath(queue, pathLen, TopSim = pathLen) */
+          for (int64_t pi = 0; pi < A.size; ++pi) {
+            int32_t target = A.cur[pi * (L + 1) + pathLen];
+            if (target == src || target == -1) continue;
+            row[(int64_t)(pathLen - 1) * n + target] = A.mass[pi * (L + 1) + pathLen];
+          }
+        }
+        if (pathLen >= L) break;
+        B.size = 0;
+        for (int64_t pi = 0; pi < A.size; ++pi) {
+          const int32_t* path = A.cur + pi * (L + 1);
+          const double* mass = A.mass + pi * (L + 1);
+          int32_t cur = path[pathLen];
+          double sm = mass[pathLen];
+          int64_t d = off[cur + 1] - off[cur];
+          if (d != 0 && sm >= (double)d) {
+            double ns = sm / (double)d;
+            pq_reserve(&B, B.size + d, L);
+            for (int64_t j = 0; j < d; ++j) {
+              int64_t c = B.size++;
+              memcpy(B.cur + c * (L + 1), path, sizeof(int32_t) * (L + 1));
+              memcpy(B.mass + c * (L + 1), mass, sizeof(double) * (L + 1));
+              B.cur[c * (L + 1) + pathLen + 1] = nbrs[off[cur] + j];
+              B.mass[c * (L + 1) + pathLen + 1] = ns;
+              B.walker[c] = A.walker[pi];
+            }
+          } else {
+            int number = (int)sm;
+            if ((double)number != sm) number += 1;
+            double ns = sm / (double)number;
+            for (int j = 0; j < number; ++j) {
+              if (d == 0) break;
+              int64_t wid = A.walker[pi] >= 0 ? A.walker[pi] : next_walker++;
+              struct gw_u4 u = gw_philox((uint32_t)src, (uint32_t)wid, (uint32_t)(pathLen + 1), call, k0, k1);
+              int64_t k = gw_bounded(u.x, (uint32_t)d);
+              pq_reserve(&B, B.size + 1, L);
+              int64_t c = B.size++;
+              memcpy(B.cur + c * (L + 1), path, sizeof(int32_t) * (L + 1));
+              memcpy(B.mass + c * (L + 1), mass, sizeof(double) * (L + 1));
+              B.cur[c * (L + 1) + pathLen + 1] = nbrs[off[cur] + k];
+              B.mass[c * (L + 1) + pathLen + 1] = ns;
+              B.walker[c] = wid;
+            }
+          }
+        }
+        pqueue tmp = A;
+        A = B;
+        B = tmp;
+      }
+    }
+    free(A.cur); free(A.mass); free(A.walker);
+    free(B.cur); free(B.mass); free(B.walker);
+  }
+}
+
+/* getSim(src, dst) of TopSim_doubleSample / TopSim_Dev (:181-193): the Java */
+/* loop order over vertices i then steps, cache[s]*P[src]*P[dst].           */
+static double levels_dot(const double* a, const double* b, int64_t n, int step, const double* cache) {
+  double result = 0.0;
+  for (int64_t i = 0; i < n; ++i)
+    for (int s = 1; s <= step; ++s) {
+      double pa = a[(int64_t)(s - 1) * n + i], pb = b[(int64_t)(s - 1) * n + i];
+      if (pa > 0.0 && pb > 0.0) result += cache[s] * pa * pb;
+    }
+  return result;
+}
+
+/* TopSim_doubleSample.computeSims (:167-176): sim[i][j] = getSim(i, j) for  */
+/* i < j, mirrored; diagonal 0.  M = or_topsim_levels over tasks (v, 0).    */
+void or_topsim_double_sims(int64_t n, const double* M, int step, double C, double* sim, int nthreads) {
+  double cache[32];
+  for (int i = 0; i <= step && i < 32; ++i) cache[i] = pow(C, (double)i);
+  memset(sim, 0, sizeof(double) * n * n);
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t j = i + 1; j < n; ++j) {
+      double v = levels_dot(M + i * step * n, M + j * step * n, n, step, cache);
+      sim[i * n + j] = v;
+      sim[j * n + i] = v;
+    }
+}
+
+/* TopSim_Dev.compute (:57-95) given the candidate lists cand[i*K + r]       */
+/* (FixedMaxPQ sortedElement order, -1 padded): sample(i) with call 0, each */
+/* candidate j = cand[i*K+r] freshly sampled with call 1 + i*K + r;         */
+/* sim[i][j] = getSim, sim[i][i] = 0.  `sample` is the derived SAMPLE.      */
+void or_topsim_dev(int64_t n, const int64_t* off, const int32_t* nbrs, int sample, int step, double C, uint64_t seed,
+                   const int32_t* cand, int K, double* sim, int nthreads) {
+  double cache[32];
+  for (int i = 0; i <= step && i < 32; ++i) cache[i] = pow(C, (double)i);
+  memset(sim, 0, sizeof(double) * n * n);
+  double* Mi = (double*)malloc(sizeof(double) * step * n);
+  double* Mj = (double*)malloc(sizeof(double) * step * n);
+  for (int64_t i = 0; i < n; ++i) {
+    int32_t tv = (int32_t)i, tc = 0;
+    or_topsim_levels(n, off, nbrs, sample, step, seed, &tv, &tc, 1, Mi, nthreads);
+    for (int r = 0; r < K; ++r) {
+      int32_t j = cand[i * K + r];
+      if (j < 0) break;
+      int32_t cv = j, cc = 1 + (int32_t)(i * K + r);
+      or_topsim_levels(n, off, nbrs, sample, step, seed, &cv, &cc, 1, Mj, nthreads);
+      sim[i * n + j] = levels_dot(Mi, Mj, n, step, cache);
+    }
+    sim[i * n + i] = 0.0;
+  }
+  free(Mi);
+  free(Mj);
+}
+
+/* DoubleRandomWalk (DoubleRandomWalk.java:50-91): SAMPLE walks of STEP      */
+/* steps per vertex (Philox (v, i, step+1)), then for every pair v < w the   */
+/* first-meeting estimator sum cache[t+1] / SAMPLE^2, mirrored.             */
+void or_double_random_walk(int64_t n, const int64_t* off, const int32_t* nbrs, int sample, int step, double C,
+                           uint64_t seed, double* sim, int nthreads) {
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32) ^ GW_TAG_TOPSIM;
+  double cache[32];
+  for (int i = 0; i <= step && i < 32; ++i) cache[i] = pow(C, (double)i);
+  int32_t* paths = (int32_t*)calloc((size_t)(n * sample * step), sizeof(int32_t));
+  for (int64_t v = 0; v < n; ++v)
+    for (int i = 0; i < sample; ++i) {
+      int32_t cur = (int32_t)v;
+      for (int t = 0; t < step; ++t) { /* sample(src) :56-65 */
+        int64_t d = off[cur + 1] - off[cur];
+        if (d == 0) {
+          cur = -1;
+        } else {
+          struct gw_u4 u = gw_philox((uint32_t)v, (uint32_t)i, (uint32_t)(t + 1), 0u, k0, k1);
+          cur = nbrs[off[cur] + gw_bounded(u.x, (uint32_t)d)];
+        }
+        paths[(v * sample + i) * step + t] = cur;
+        if (cur == -1) break;
+      }
+    }
+  memset(sim, 0, sizeof(double) * n * n);
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int64_t v = 0; v < n; ++v)
+    for (int64_t w = v + 1; w < n; ++w) {
+      double result = 0.0;
+      for (int i = 0; i < sample; ++i)
+        for (int j = 0; j < sample; ++j) {
+          const int32_t* a = paths + (v * sample + i) * step;
+          const int32_t* b = paths + (w * sample + j) * step;
+          for (int t = 0; t < step && a[t] != -1 && b[t] != -1; ++t)
+            if (a[t] == b[t]) {
+              result += cache[t + 1];
+              break;
+            }
+        }
+      double val = result / ((double)sample * (double)sample);
+      sim[v * n + w] = val;
+      sim[w * n + v] = val;
+    }
+  free(paths);
+}
+
 /* FixedCacheMap.main (FixedCacheMap.java:134-148) as a known-answer check:  */
 /* puts (key, value) in order into a map of capacity nmax, drains ascending. */
 int or_fcm_run(int nmax, int64_t nput, const int32_t* keys, const float* vals, int32_t* ok, float* ov) {

@@ -197,3 +197,17 @@ def test_compute_calls_fail_loudly_without_gpu(gw):
     out = np.zeros(34 * 34)
     with pytest.raises(C.StateError):
         C.check(C.lib().gw_simrank_naive_host(G.handle, 0.6, 3, C.ptr(out)), G.handle)
+
+
+def test_select_fixed_max_pq_for_topsim_dev(gw, oracle):
+    """TopSim_Dev's candidate choice (TopSim_Dev.java:64-71): FixedMaxPQ over
+    entries >= MIN in j order, sortedElement() order (ties included)."""
+    from gwamd import topsim
+    rng = np.random.RandomState(3)
+    cand = np.round(rng.rand(30, 41) * 6) / 6
+    cand[cand < 0.2] = 1e-12  # below MyConfiguration.MIN
+    cand[4] = 0.0
+    ids = topsim.select_candidates(cand, 7)
+    for i in range(30):
+        exp = [j for j, _ in oracle.java_fixed_max_pq_row(cand[i], 7, min_score=topsim.MIN)]
+        assert ids[i].tolist() == exp + [-1] * (7 - len(exp))

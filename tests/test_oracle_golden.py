@@ -283,3 +283,58 @@ def test_topsim_m_oracle_no_eviction_matches_topsim(oracle):
         assert set(ks.tolist()) == set(np.nonzero(rows[r])[0].tolist())
         np.testing.assert_allclose(vals[r, :size[r]], rows[r][ks] / 300, rtol=1e-5)
         assert np.all(np.diff(vals[r, :size[r]]) >= 0)  # ascending iteration
+
+
+def _py_double_sample_levels(adj, src, SAMPLE, STEP):
+    """Literal Python port of TopSim_doubleSample.sample/computePath
+    (TopSim_doubleSample.java:71-164) for the deterministic regime (every
+    queued path has mass >= degree, so no randNeighbor call happens)."""
+    from collections import deque
+    P = {}
+    queue = deque([[(src, float(SAMPLE))]])
+    pathLen, TopSim = 0, 1
+
+    def computePath(step):
+        for path in queue:
+            target = path[step][0]
+            if target == src:
+                continue
+            P[(target, step)] = path[step][1]
+
+    while pathLen < STEP:
+        if pathLen == TopSim:
+            computePath(pathLen)
+            TopSim += 1
+        for _ in range(len(queue)):
+            path = queue[0]
+            cur, sample = path[pathLen]
+            degree = len(adj[cur])
+            assert degree != 0 and sample >= degree, "deterministic regime only"
+            newSample = sample / degree
+            for j in range(degree):
+                queue.append(path + [(adj[cur][j], newSample)])
+            queue.popleft()
+        pathLen += 1
+    computePath(pathLen)
+    return P
+
+
+def test_double_sample_levels_deterministic_kat(oracle):
+    """or_topsim_levels == the literal Java-queue port (last path wins) on
+    karate (Java multigraph semantics) with SAMPLE large enough that every
+    path is enumerated."""
+    path = os.path.join(DATA, "karate.edgelist")
+    adj = [[] for _ in range(35)]
+    with open(path) as f:
+        for line in f:
+            a, b = line.split()[:2]
+            adj[int(a)].append(int(b))
+            adj[int(b)].append(int(a))
+    offs = np.zeros(36, np.int64)
+    offs[1:] = np.cumsum([len(x) for x in adj])
+    nbrs = np.array([y for x in adj for y in x], np.int32)
+    M = oracle.topsim_levels(offs, nbrs, 10 ** 6, 3, np.arange(1, 35, dtype=np.int32))
+    for t, src in enumerate(range(1, 35)):
+        P = _py_double_sample_levels(adj, src, 10 ** 6, 3)
+        got = {(x, s + 1): M[t, s, x] for s in range(3) for x in range(35) if M[t, s, x] > 0}
+        assert got == P
