@@ -29,7 +29,8 @@ struct gw_bs_nbr {  // GW_N2V_BITSET: one 64 B entry (one HBM sector) per adjace
   uint32_t kp, c;                // position of u in N(x), #common neighbours
   uint32_t w[10];                // payload, by (c, d): c <= 20 && d < 65536: positions of the
                                  // common neighbours (u16, ascending, 0xFFFF padded); else
-                                 // d <= 320: the bitset itself; else w[0..1] = region word offset
+                                 // d <= 320: the bitset itself; else Elias-Fano positions when
+                                 // they fit in 320 bits; else w[0..1] = region word offset
 };
 #if defined(__HIPCC__)
 #define GW_HD __host__ __device__
@@ -37,6 +38,18 @@ struct gw_bs_nbr {  // GW_N2V_BITSET: one 64 B entry (one HBM sector) per adjace
 #define GW_HD
 #endif
 GW_HD inline bool gw_bs_is_list(uint32_t c, uint32_t d) { return c <= GW_BS_LIST && d < 65536u; }
+// Elias-Fano payload (neither list nor inline bitset): l low bits per
+// position, then the unary high parts; fits when c*l + c + ((d-1)>>l) + 1 <= 320.
+GW_HD inline int gw_bs_ef_l(uint32_t c, uint32_t d) {
+  int l = 0;
+  while (c > 0 && ((uint64_t)c << (l + 1)) <= (uint64_t)d) ++l;  // floor(log2(d / c))
+  return l;
+}
+GW_HD inline bool gw_bs_is_ef(uint32_t c, uint32_t d) {
+  if (gw_bs_is_list(c, d) || d <= (uint32_t)GW_BS_INLINE_BITS || c == 0) return false;
+  const int l = gw_bs_ef_l(c, d);
+  return (uint64_t)c * l + c + ((d - 1) >> l) + 1 <= (uint64_t)GW_BS_INLINE_BITS;
+}
 static_assert(sizeof(gw_bs_nbr) == 64, "bitset entry must be one 64 B sector");
 
 struct gw_dev_graph {
