@@ -211,16 +211,16 @@ __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff
     } else if (gw_bs_is_ef(c, (uint32_t)d) && lane == 0) {
       // Elias-Fano from the region bits lane 0 wrote above (same thread: visible)
       const int l = gw_bs_ef_l(c, (uint32_t)d);
-      const int B0 = (int)c * l;
+      const uint32_t U = c + (uint32_t)((d - 1) >> l) + 1;
       uint32_t ef[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
       uint32_t idx = 0;
       for (int64_t w = 0; w < (d + 31) / 32; ++w)
         for (uint32_t x = bits[w]; x; x &= x - 1) {
           const uint32_t p = (uint32_t)(32 * w + __ffs(x) - 1);
-          for (int b = 0; b < l; ++b)
-            if ((p >> b) & 1u) ef[(idx * l + b) >> 5] |= 1u << ((idx * l + b) & 31);
-          const uint32_t up = (uint32_t)B0 + (p >> l) + idx;
+          const uint32_t up = (p >> l) + idx;  // high part, unary
           ef[up >> 5] |= 1u << (up & 31);
+          for (int b = 0; b < l; ++b)
+            if ((p >> b) & 1u) ef[(U + idx * l + b) >> 5] |= 1u << ((U + idx * l + b) & 31);
           ++idx;
         }
       for (int t = 0; t < 10; ++t) bsn[e].w[t] = ef[t];
@@ -310,30 +310,18 @@ __device__ __forceinline__ uint32_t pick10(const uint32_t (&pl)[10], uint32_t id
   return r;
 }
 
-// ---- Elias-Fano payload (registers, constant indices only) ----------------
-// mask of the bits of word t at global positions in [lo, hi)
-__device__ __forceinline__ uint32_t ef_mask(int t, int lo, int hi) {
-  const int a = max(lo - 32 * t, 0), b = min(hi - 32 * t, 32);
-  if (a >= b) return 0u;
-  const uint32_t upto = b >= 32 ? 0xFFFFFFFFu : ((1u << b) - 1u);
-  return upto & ~((a >= 32) ? 0xFFFFFFFFu : ((1u << a) - 1u));
-}
-__device__ __forceinline__ uint32_t ef_low(const uint32_t (&pl)[10], uint32_t i, int l) {
-  if (l == 0) return 0u;
-  const uint32_t off = i * (uint32_t)l;
-  const uint32_t w = off >> 5, sh = off & 31;
-  const uint64_t v = ((uint64_t)pick10(pl, w + 1) << 32) | pick10(pl, w);
-  return (uint32_t)(v >> sh) & ((1u << l) - 1u);
-}
-// position of the j-th one (ONE = true) or zero among bits [B0, B0+U), relative to B0; -1 if none
+// ---- Elias-Fano payload ----------------------------------------------------
+// The payload words live in registers; dynamic word picks are mask-selects.
+// j-th one (ONE) / zero among the payload bits, from bit 0 (the high parts
+// come first, so the first c ones and the first U - c zeros are theirs)
 template <bool ONE>
-__device__ __forceinline__ int ef_select_bit(const uint32_t (&pl)[10], int B0, int U, uint32_t j) {
+__device__ __forceinline__ int ef_select_bit(const uint32_t (&pl)[10], uint32_t j) {
   uint32_t x = 0;
   int base = 0;
   bool found = false;
 #pragma unroll
   for (int t = 0; t < 10; ++t) {
-    const uint32_t m = (ONE ? pl[t] : ~pl[t]) & ef_mask(t, B0, B0 + U);
+    const uint32_t m = ONE ? pl[t] : ~pl[t];
     const uint32_t pc = (uint32_t)__popc(m);
     if (!found) {
       if (j < pc) {
@@ -345,32 +333,27 @@ __device__ __forceinline__ int ef_select_bit(const uint32_t (&pl)[10], int B0, i
       }
     }
   }
-  return found ? base + word_select(x, j) - B0 : -1;
+  return base + word_select(x, j);
 }
-// j-th smallest common-neighbour position
-__device__ __forceinline__ int64_t ef_select(const uint32_t (&pl)[10], uint32_t c, uint32_t d, uint32_t j) {
-  const int l = gw_bs_ef_l(c, d);
-  const int B0 = (int)c * l;
-  const int U = (int)c + (int)((d - 1) >> l) + 1;
-  const int pos = ef_select_bit<true>(pl, B0, U, j);
-  return ((int64_t)(uint32_t)(pos - (int)j) << l) | ef_low(pl, j, l);
+__device__ __forceinline__ uint32_t ef_low(const uint32_t (&pl)[10], uint32_t U, uint32_t i, int l) {
+  if (l == 0) return 0u;
+  const uint32_t off = U + i * (uint32_t)l;
+  const uint32_t w = off >> 5, sh = off & 31;
+  const uint64_t v = ((uint64_t)pick10(pl, w + 1) << 32) | pick10(pl, w);
+  return (uint32_t)(v >> sh) & ((1u << l) - 1u);
 }
-// is k one of the positions?
-__device__ __forceinline__ bool ef_has(const uint32_t (&pl)[10], uint32_t c, uint32_t d, uint32_t k) {
-  const int l = gw_bs_ef_l(c, d);
-  const int B0 = (int)c * l;
-  const int U = (int)c + (int)((d - 1) >> l) + 1;
+__device__ __forceinline__ int64_t ef_select(const uint32_t (&pl)[10], uint32_t U, int l, uint32_t j) {
+  const int pos = ef_select_bit<true>(pl, j);
+  return ((int64_t)(uint32_t)(pos - (int)j) << l) | ef_low(pl, U, j, l);
+}
+__device__ __forceinline__ bool ef_has(const uint32_t (&pl)[10], uint32_t c, uint32_t U, int l, uint32_t k) {
   const uint32_t h = k >> l, lowk = k & ((1u << l) - 1u);
-  int s = 0;  // bucket h starts right after the (h-1)-th zero
-  if (h > 0) {
-    const int z = ef_select_bit<false>(pl, B0, U, h - 1);
-    if (z < 0) return false;
-    s = z + 1;
-  }
-  for (int q = s; q < U; ++q) {
-    const uint32_t g = (uint32_t)(B0 + q);
-    if (!((pick10(pl, g >> 5) >> (g & 31)) & 1u)) break;
-    if (ef_low(pl, (uint32_t)(q - (int)h), l) == lowk) return true;
+  if (h > U - c) return false;  // beyond the largest high part
+  // bucket h starts right after the (h-1)-th zero
+  const uint32_t s = h > 0 ? (uint32_t)ef_select_bit<false>(pl, h - 1) + 1 : 0u;
+  for (uint32_t q = s; q < U; ++q) {
+    if (!((pick10(pl, q >> 5) >> (q & 31)) & 1u)) break;
+    if (ef_low(pl, U, q - h, l) == lowk) return true;
   }
   return false;
 }
@@ -395,6 +378,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
   __shared__ int32_t s_stage[kB / 64][kStage][64];
   const int lane = threadIdx.x & 63;
   int32_t* stage = &s_stage[threadIdx.x >> 6][0][lane];
+
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long my_steps = 0, my_trials = 0;
   if (i < walk_count) {
@@ -417,6 +401,8 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
     int64_t b = G.offsets[cur], d = G.offsets[cur + 1] - b;  // row of cur
     uint32_t c = 0, kp = 0, boff = 0;
     bool inl = true, lst = false, efm = false;
+    uint32_t efU = 0;
+    int efl = 0;
     uint32_t pl[10];  // entry payload: the common-neighbour list in list mode
 #pragma unroll
     for (int t = 0; t < 10; ++t) pl[t] = 0xFFFFFFFFu;
@@ -439,14 +425,14 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
           k = (P.diag & 1) ? (int64_t)((uint64_t)j * (uint64_t)d / c)
               : lst        ? (int64_t)((pick10(pl, j >> 1) >> (16 * (j & 1))) & 0xFFFFu)
               : inl        ? (int64_t)regs_select<10>(pl, j)
-              : efm        ? ef_select(pl, c, (uint32_t)d, j)
+              : efm        ? ef_select(pl, efU, efl, j)
                            : bs_select(h, d, c, j);
         } else {
           k = (int64_t)gw_bounded(u.y, (uint32_t)d);
           const bool common = (P.diag & 2) ? false
                               : lst ? list_has(pl, (uint32_t)k)
                               : inl ? ((pick10(pl, (uint32_t)(k >> 5)) >> (k & 31)) & 1u)
-                              : efm ? ef_has(pl, c, (uint32_t)d, (uint32_t)k)
+                              : efm ? ef_has(pl, c, efU, efl, (uint32_t)k)
                                     : ((h[boff + (k >> 5)] >> (k & 31)) & 1u);
           acc = (k != (int64_t)kp) && !common;
         }
@@ -454,7 +440,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
         k = (int64_t)gw_bounded(u.y, (uint32_t)d);
         const bool common = lst ? list_has(pl, (uint32_t)k)
                             : inl ? ((pick10(pl, (uint32_t)(k >> 5)) >> (k & 31)) & 1u)
-                            : efm ? ef_has(pl, c, (uint32_t)d, (uint32_t)k)
+                            : efm ? ef_has(pl, c, efU, efl, (uint32_t)k)
                                   : ((h[boff + (k >> 5)] >> (k & 31)) & 1u);
         acc = ((k != (int64_t)kp) && !common) || trial >= (1u << 24);
       }
@@ -473,10 +459,15 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
         lst = gw_bs_is_list(c, (uint32_t)d);
         inl = !lst && d <= GW_BS_INLINE_BITS;
         efm = gw_bs_is_ef(c, (uint32_t)d);
+        if (efm) {
+          efl = gw_bs_ef_l(c, (uint32_t)d);
+          efU = c + (uint32_t)((d - 1) >> efl) + 1;
+        }
         h = (lst || inl || efm) ? en->w : G.bs_region + ((uint64_t)e1.z | ((uint64_t)e1.w << 32));
         boff = (uint32_t)bs_boff(d);
         pl[0] = e1.z; pl[1] = e1.w; pl[2] = e2.x; pl[3] = e2.y; pl[4] = e2.z;
         pl[5] = e2.w; pl[6] = e3.x; pl[7] = e3.y; pl[8] = e3.z; pl[9] = e3.w;
+
         stage[64 * (len & (kStage - 1))] = cur;
         if ((len & (kStage - 1)) == kStage - 1) {
           int32_t* dst = row + (len - (kStage - 1));
