@@ -1,0 +1,106 @@
+"""Full-size checks at BASELINE.json's bench configurations, through
+size-independent properties plus oracle parity on windows of the same run:
+
+* config 2 (the headline): node2vec p=0.25 q=4, L=80, 10 walks per vertex on
+  the Graph500 R-MAT scale-20 graph, GW_N2V_BITSET — every step follows an
+  edge, every iteration starts every vertex once, shard invariance, counters,
+  and bit-exact oracle parity on walk windows;
+* config 5: TopSim_singleSample on the 10M-vertex Java-semantics R-MAT graph
+  (STEP 3, SAMPLE 1000, top-100) — oracle parity for sampled sources and the
+  top-k invariants for a block of sources."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _is_edge(offs, nbrs, a, b):
+    lo, hi = offs[a], offs[a + 1]
+    ok = np.zeros(len(a), bool)
+    for idx in range(len(a)):  # rows are sorted by dense id
+        r = nbrs[lo[idx]:hi[idx]]
+        j = np.searchsorted(r, b[idx])
+        ok[idx] = j < len(r) and r[j] == b[idx]
+    return ok
+
+
+def test_headline_config_bitset_walks(gw, oracle):
+    import torch
+    from gwamd import _lib as C
+    G = gw.GWGraph.rmat(20, 16, 0.57, 0.19, 0.19, 42).to_device(0)
+    C.check(C.lib().gw_n2v_prepare(G.handle, 0.25, 4.0, C.N2V_BITSET), G.handle)
+    n, L, R = G.n, 80, 10
+    tot = n * R
+    out = torch.empty((tot, L), dtype=torch.int32, device="cuda")
+    lens = torch.empty(tot, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    C.check(C.lib().gw_n2v_walks(G.handle, L, 42, 0, tot, 1, C.ptr(out), C.ptr(lens), C.ptr(cnt), None), G.handle)
+    torch.cuda.synchronize()
+    csr = G.export_csr()
+    offs, nbrs = csr["offsets"], csr["nbrs"]
+    deg = np.diff(offs)
+    # every iteration starts every vertex exactly once
+    starts = out[:, 0].cpu().numpy()
+    for it in (0, R - 1):
+        np.testing.assert_array_equal(np.sort(starts[it * n:(it + 1) * n]), np.arange(n))
+    # lengths: L for non-isolated starts (undirected: no dead ends), 1 otherwise
+    ln = lens.cpu().numpy()
+    np.testing.assert_array_equal(ln, np.where(deg[starts] > 0, L, 1))
+    assert int(cnt[0].item()) == int((ln - 1).sum())
+    assert 1.0 <= int(cnt[1].item()) / int(cnt[0].item()) < 1.2  # rejection trials per step
+    # sampled steps follow edges
+    rng = np.random.default_rng(0)
+    rows = rng.integers(0, tot, 2000)
+    W = out[torch.as_tensor(rows, device="cuda")].cpu().numpy()
+    W = W[ln[rows] == L]
+    a, b = W[:, :-1].ravel(), W[:, 1:].ravel()
+    assert _is_edge(offs, nbrs, a, b).all()
+    # oracle parity on windows of the same run (a pure function of the walk index)
+    for begin in (0, tot // 2 + 12345):
+        ref, rl, _ = oracle.walks_bitset(csr, 0.25, 4.0, 42, L, begin, 1500, nthreads=8)
+        np.testing.assert_array_equal(out[begin:begin + 1500].cpu().numpy(), ref)
+        np.testing.assert_array_equal(ln[begin:begin + 1500], rl)
+    # shard invariance: a window computed on its own equals the same rows of the full run
+    part = torch.empty((3000, L), dtype=torch.int32, device="cuda")
+    C.check(C.lib().gw_n2v_walks(G.handle, L, 42, 5 * n - 1000, 3000, 1, C.ptr(part), None, None, None), G.handle)
+    torch.cuda.synchronize()
+    assert torch.equal(part, out[5 * n - 1000:5 * n + 2000])
+
+
+def test_p10m_topsim_sources(gw, oracle):
+    import torch
+    from gwamd import _lib as C
+    pg = gw.GWGraph.rmat_java(10_000_000, 100_000_000, 0.57, 0.19, 0.19, 42)
+    csr = pg.export_csr()
+    offs, nbrs = csr["offsets"], csr["nbrs"]
+    deg = np.diff(offs)
+    pg.to_device(0)
+    K, sample, step = 100, 1000, 3
+    nz = np.nonzero(deg > 0)[0]
+    rng = np.random.default_rng(1)
+    pick = np.concatenate([nz[np.argsort(deg[nz])[-4:]], rng.choice(nz, 60, replace=False)]).astype(np.int32)
+    src = torch.as_tensor(pick, device="cuda")
+    ids = torch.empty((len(pick), K), dtype=torch.int32, device="cuda")
+    sc = torch.empty((len(pick), K), dtype=torch.float64, device="cuda")
+    st = torch.zeros(4, dtype=torch.int64, device="cuda")
+    C.check(C.lib().gw_topsim(pg.handle, C.TOPSIM_SINGLE_SAMPLE, sample, step, 0.6, 42, C.ptr(src), len(pick), K,
+                              C.ptr(ids), C.ptr(sc), C.ptr(st), None), pg.handle)
+    torch.cuda.synchronize()
+    I, S = ids.cpu().numpy(), sc.cpu().numpy()
+    # oracle rows (dense over 10M vertices per source is too large: compare on the top-k support)
+    for r, s in enumerate(pick[:16]):
+        rows, _ = oracle.topsim(offs, nbrs, 0, sample, step, C=0.6, seed=42, sources=np.array([s], np.int32),
+                                nthreads=8)
+        row = rows[0]
+        nz = np.nonzero(row > 0)[0]
+        top = nz[np.lexsort((nz, -row[nz]))][:K]
+        got = I[r][I[r] >= 0]
+        assert len(got) == len(top)
+        np.testing.assert_allclose(S[r, :len(top)], row[top], rtol=1e-12)
+        for a, b in zip(got, top):  # ids equal except where scores tie within fp noise
+            if a != b:
+                assert abs(row[a] - row[b]) <= 1e-12 * row[b]
+    # invariants for every sampled source: sorted desc, no self, ids valid
+    for r, s in enumerate(pick):
+        k = int((I[r] >= 0).sum())
+        assert np.all(np.diff(S[r, :k]) <= 0) and s not in I[r, :k] and np.all(S[r, :k] > 0)
