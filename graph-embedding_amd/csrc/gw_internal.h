@@ -67,16 +67,24 @@ struct gw_dev_graph {
   gw_bs_nbr* bs_nbr = nullptr;    // [nnz] neighbour + region offset
 };
 
+struct gw_ts_ent {  // TopSim adjacency slot (u -> x): everything a walker's next step needs
+  int32_t x, d;      // neighbour, deg(x)
+  int64_t off;       // offsets[x]
+};
+
 struct gw_topsim_ws {
   int variant = -1, sample = 0, step = 0, topk = 0;
   int blocks = 0;               // persistent workgroups
   int64_t level_cap = 0;        // records per level per workgroup
   int64_t spawn_cap = 0;        // spawner records per workgroup
   int64_t touch_cap = 0;        // distinct targets per workgroup
-  int lds_row = 0;              // accumulator row lives in LDS
+  int lds_row = 0;              // accumulator: 0 dense LDS row, 1 LDS hash (8192 slots)
   size_t lds_bytes = 0;         // dynamic LDS per workgroup
   int32_t* lvl_vertex = nullptr;  // [blocks][levels][level_cap]
   int32_t* lvl_parent = nullptr;  // [blocks][levels][level_cap]
+  int32_t* lvl_deg = nullptr;     // [blocks][levels][level_cap] deg(vertex)
+  int64_t* lvl_off = nullptr;     // [blocks][levels][level_cap] offsets[vertex]
+  gw_ts_ent* ent = nullptr;       // [nnz] slot entries (built once per graph)
   double* lvl_mass = nullptr;     // [blocks][2][level_cap] (current/next)
   int32_t* child_off = nullptr;   // [blocks][level_cap+1] expansion scan
   int32_t* spawn_node = nullptr;  // [blocks][spawn_cap] index into its level

@@ -408,6 +408,9 @@ void gw_dev_release(gw_graph* g) {
   gw_topsim_ws& t = g->ts;
   dev_free(t.lvl_vertex);
   dev_free(t.lvl_parent);
+  dev_free(t.lvl_deg);
+  dev_free(t.lvl_off);
+  dev_free(t.ent);
   dev_free(t.lvl_mass);
   dev_free(t.child_off);
   dev_free(t.spawn_node);

@@ -39,9 +39,6 @@ constexpr int TS_BLOCK = 512;
 constexpr int TS_WAVES = TS_BLOCK / 64;
 constexpr int TOPK_MAX = 256;
 constexpr int64_t LDS_ROW_MAX_BYTES = 96 * 1024;
-constexpr int HASH_BITS = 13;                 // LDS hash: 8192 slots = 96 KB
-constexpr int HASH_SLOTS = 1 << HASH_BITS;
-constexpr int HASH_LIMIT = HASH_SLOTS * 3 / 4;  // load limit before overflowing to HBM
 
 struct TsArgs {
   gw_dev_graph G;
@@ -60,6 +57,9 @@ struct TsArgs {
   int64_t level_cap, spawn_cap, touch_cap;
   int32_t* lvl_vertex;
   int32_t* lvl_parent;
+  int32_t* lvl_deg;
+  int64_t* lvl_off;
+  const gw_ts_ent* ent;
   double* lvl_mass;
   int32_t* child_off;
   int32_t* spawn_node;
@@ -127,8 +127,13 @@ __device__ __forceinline__ unsigned long long dkey(double v) {
   return (unsigned long long)__double_as_longlong(v);  // v >= 0: bit order == value order
 }
 
-template <int STEP, bool LDS_ROW>
+// MODE 0: dense LDS row; 1: LDS hash of 8192 slots (96 KB)
+template <int STEP, int MODE>
 __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
+  constexpr bool LDS_ROW = MODE == 0;
+  constexpr int HASH_BITS = 13;
+  constexpr int HASH_SLOTS = 1 << HASH_BITS;
+  constexpr int HASH_LIMIT = HASH_SLOTS * 3 / 4;  // load limit before overflowing to HBM
   constexpr int L = 2 * STEP;
   extern __shared__ double s_row[];  // LDS row (LDS_ROW) or hash values+keys
   __shared__ int s_wave[TS_WAVES + 1];
@@ -147,6 +152,8 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
   const int64_t cap = A.level_cap;
   int32_t* V = A.lvl_vertex + blk * (int64_t)(L + 1) * cap;
   int32_t* P = A.lvl_parent + blk * (int64_t)(L + 1) * cap;
+  int32_t* D = A.lvl_deg + blk * (int64_t)(L + 1) * cap;
+  int64_t* O = A.lvl_off + blk * (int64_t)(L + 1) * cap;
   double* M = A.lvl_mass + blk * 2 * cap;
   int32_t* CO = A.child_off + blk * (cap + 1);
   int32_t* SN = A.spawn_node + blk * A.spawn_cap;
@@ -228,14 +235,15 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
   };
 
   // computePathSim for the path node at depth 2i with mass `mass`
-  auto contrib = [&](const int32_t* path, int i, int32_t source, double mass) {
+  // (degrees travel with the path: dpath[t] = deg(path[t]))
+  auto contrib = [&](const int32_t* path, const int32_t* dpath, int i, int32_t source, double mass) {
     const int32_t target = path[2 * i];
     if (target == source) return;  // TopSim_singleSample.java:183
 #pragma unroll
     for (int j = 0; j < STEP; ++j)  // isFirstMeet (:211-218)
       if (j < i && path[j] == path[2 * i - j]) return;
-    const double dm = (double)G.deg[path[i]];
-    const double dt = (double)G.deg[target];
+    const double dm = (double)dpath[i];
+    const double dt = (double)dpath[2 * i];
     double val;
     if (rw)  // SingleRandomWalk.java:89: cache[i]*deg/deg/SAMPLE
       val = ((A.cache[i] * dm) / dt) / A.sampled;
@@ -274,6 +282,8 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
     } else {
       if (tid == 0) {
         V[0] = s;
+        D[0] = ds;
+        O[0] = G.offsets[s];
         P[0] = -1;
         M[0] = A.sampled;  // path[0].sample = SAMPLE (:73)
         s_size[0] = 1;
@@ -288,19 +298,21 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
         // computePathSim at pathLen = 2i (:80-83, :157) for enumerated nodes
         if ((l & 1) == 0 && l >= 2) {
           for (int j = tid; j < sz; j += TS_BLOCK) {
-            int32_t path[L + 1];
+            int32_t path[L + 1], dpath[L + 1];
             int p = j;
 #pragma unroll
             for (int t = L; t >= 1; --t) {
               if (t <= l) {
                 path[t] = V[(int64_t)t * cap + p];
+                dpath[t] = D[(int64_t)t * cap + p];
                 p = P[(int64_t)t * cap + p];
               }
             }
             path[0] = s;
+            dpath[0] = ds;
 #pragma unroll
             for (int t = 2; t <= L; t += 2)
-              if (t == l) contrib(path, t / 2, s, Ml[j]);
+              if (t == l) contrib(path, dpath, t / 2, s, Ml[j]);
           }
         }
         if (l == L) break;
@@ -312,8 +324,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
           int cnt = 0, sp = 0;
           double m = 0.0;
           if (j < sz) {
-            const int32_t v = Vl[j];
-            const int d = G.deg[v];
+            const int d = D[(int64_t)l * cap + j];
             m = Ml[j];
             const bool det = enumerate_all ? (d != 0) : (d != 0 && m >= (double)d);  // :99
             if (det)
@@ -357,12 +368,17 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
         int32_t* Vn = V + (int64_t)(l + 1) * cap;
         int32_t* Pn = P + (int64_t)(l + 1) * cap;
         double* Mn = M + (int64_t)((l + 1) & 1) * cap;
+        int32_t* Dn = D + (int64_t)(l + 1) * cap;
+        int64_t* On = O + (int64_t)(l + 1) * cap;
+        const int64_t* Ol = O + (int64_t)l * cap;
         for (int c = tid; c < total_children; c += TS_BLOCK) {
           const int j = upper_bound_i32(CO, sz + 1, c) - 1;
-          const int32_t v = Vl[j];
           const int k = c - CO[j];
           const int d = CO[j + 1] - CO[j];
-          Vn[c] = G.nbrs[G.offsets[v] + k];  // edges.get(j), insertion order (:103-110)
+          const gw_ts_ent e = A.ent[Ol[j] + k];  // edges.get(j), insertion order (:103-110)
+          Vn[c] = e.x;
+          Dn[c] = e.d;
+          On[c] = e.off;
           Pn[c] = j;
           Mn[c] = Ml[j] / (double)d;         // newSample = cur.sample / degree (:104)
         }
@@ -399,33 +415,38 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
         const int sp = upper_bound_i32(SF, ns + 1, g) - 1;
         const int l0 = SL[sp];
         const double mw = SM[sp];
-        int32_t path[L + 1];
+        int32_t path[L + 1], dpath[L + 1];
         int p = SN[sp];
+        int32_t dcur = ds;
+        int64_t ocur = rw ? G.offsets[s] : (l0 == 0 ? O[0] : O[(int64_t)l0 * cap + p]);
 #pragma unroll
         for (int t = L; t >= 1; --t) {
           if (t <= l0) {
             path[t] = V[(int64_t)t * cap + p];
+            dpath[t] = D[(int64_t)t * cap + p];
             p = P[(int64_t)t * cap + p];
           }
         }
         path[0] = s;
-        int32_t cur = s;
+        dpath[0] = ds;
 #pragma unroll
         for (int t = 0; t <= L; ++t)
-          if (t == l0) cur = path[t];
+          if (t == l0) dcur = dpath[t];
         bool alive = true;
 #pragma unroll
         for (int t = 1; t <= L; ++t) {
           if (t > l0 && alive) {
-            const int d = G.deg[cur];
-            if (d == 0) {
+            if (dcur == 0) {
               alive = false;
             } else {
               gw_u4 u = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)t, 0u, A.k0, A.k1);
-              cur = G.nbrs[G.offsets[cur] + gw_bounded(u.x, (uint32_t)d)];  // randNeighbor
-              path[t] = cur;
+              const gw_ts_ent e = A.ent[ocur + gw_bounded(u.x, (uint32_t)dcur)];  // randNeighbor
+              path[t] = e.x;
+              dpath[t] = e.d;
+              dcur = e.d;
+              ocur = e.off;
               ++my_ext;
-              if ((t & 1) == 0) contrib(path, t / 2, s, mw);
+              if ((t & 1) == 0) contrib(path, dpath, t / 2, s, mw);
             }
           }
         }
@@ -672,13 +693,24 @@ int ws_alloc(gw_graph* g, T** p, int64_t count) {
   return GW_OK;
 }
 
+__global__ void k_ts_ent(gw_dev_graph G, gw_ts_ent* __restrict__ ent) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= G.nnz) return;
+  const int32_t x = G.nbrs[e];
+  gw_ts_ent v;
+  v.x = x;
+  v.d = G.deg[x];
+  v.off = G.offsets[x];
+  ent[e] = v;
+}
+
 template <typename T>
 void ws_free(T*& p) {
   if (p) (void)hipFree(p);
   p = nullptr;
 }
 
-template <int STEP, bool LDS>
+template <int STEP, int LDS>
 hipError_t launch_step(const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
   {
     hipError_t e = hipFuncSetAttribute((const void*)k_topsim<STEP, LDS>,
@@ -689,7 +721,7 @@ hipError_t launch_step(const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <bool LDS>
+template <int LDS>
 hipError_t launch(int step, const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
   switch (step) {
     case 1: return launch_step<1, LDS>(A, blocks, lds, s);
@@ -727,6 +759,8 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   gw_topsim_ws& t = g->ts;
   ws_free(t.lvl_vertex);
   ws_free(t.lvl_parent);
+  ws_free(t.lvl_deg);
+  ws_free(t.lvl_off);
   ws_free(t.lvl_mass);
   ws_free(t.child_off);
   ws_free(t.spawn_node);
@@ -755,6 +789,7 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
     return GW_ERR_INVALID;
   }
   const bool lds_row = n * 8 <= LDS_ROW_MAX_BYTES;
+  const int mode = lds_row ? 0 : 1;
   // hash mode: HBM overflow table per workgroup (power of two) beyond the
   // 6144 keys the LDS table holds; distinct targets per source are bounded by
   // min(n, pair updates <= ~3*STEP*SAMPLE)
@@ -764,7 +799,7 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
     touch_cap = 1;
     while (touch_cap < want) touch_cap <<= 1;
   }
-  const int64_t per_block = (int64_t)(L + 1) * level_cap * 8 + 2 * level_cap * 8 + (level_cap + 1) * 4 +
+  const int64_t per_block = (int64_t)(L + 1) * level_cap * 20 + 2 * level_cap * 8 + (level_cap + 1) * 4 +
                             spawn_cap * 20 + 4 + (lds_row ? 0 : touch_cap * 16);
   int dev_cus = 256;
   hipDeviceProp_t prop;
@@ -779,6 +814,8 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   int rc;
   if ((rc = ws_alloc(g, &t.lvl_vertex, blocks * (L + 1) * level_cap)) ||
       (rc = ws_alloc(g, &t.lvl_parent, blocks * (L + 1) * level_cap)) ||
+      (rc = ws_alloc(g, &t.lvl_deg, blocks * (L + 1) * level_cap)) ||
+      (rc = ws_alloc(g, &t.lvl_off, blocks * (L + 1) * level_cap)) ||
       (rc = ws_alloc(g, &t.lvl_mass, blocks * 2 * level_cap)) ||
       (rc = ws_alloc(g, &t.child_off, blocks * (level_cap + 1))) ||
       (rc = ws_alloc(g, &t.spawn_node, blocks * spawn_cap)) ||
@@ -788,6 +825,11 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
       (rc = ws_alloc(g, &t.touched, blocks * touch_cap)) ||
       (rc = ws_alloc(g, &t.src_counter, 1)) || (rc = ws_alloc(g, &t.error_flag, 1)))
     return rc;
+  if (!t.ent && g->nnz > 0) {  // slot entries {x, deg(x), offsets[x]}: one random line per path extension
+    if ((rc = ws_alloc(g, &t.ent, g->nnz))) return rc;
+    k_ts_ent<<<(unsigned)((g->nnz + 255) / 256), 256>>>(g->d, t.ent);
+    GW_HIP_TRY(hipGetLastError());
+  }
   if (!lds_row) {
     if ((rc = ws_alloc(g, &t.acc_row, blocks * touch_cap)) || (rc = ws_alloc(g, &t.ov_keys, blocks * touch_cap)))
       return rc;
@@ -802,8 +844,8 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   t.level_cap = level_cap;
   t.spawn_cap = spawn_cap;
   t.touch_cap = touch_cap;
-  t.lds_row = lds_row ? 1 : 0;
-  t.lds_bytes = lds_row ? (size_t)n * 8 : (size_t)HASH_SLOTS * 12;
+  t.lds_row = mode;
+  t.lds_bytes = lds_row ? (size_t)n * 8 : (size_t)8192 * 12;
   GW_HIP_TRY(hipDeviceSynchronize());
   return GW_OK;
 }
@@ -841,6 +883,9 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   A.touch_cap = t.touch_cap;
   A.lvl_vertex = t.lvl_vertex;
   A.lvl_parent = t.lvl_parent;
+  A.lvl_deg = t.lvl_deg;
+  A.lvl_off = t.lvl_off;
+  A.ent = t.ent;
   A.lvl_mass = t.lvl_mass;
   A.child_off = t.child_off;
   A.spawn_node = t.spawn_node;
@@ -855,8 +900,8 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   GW_HIP_TRY(hipMemsetAsync(t.src_counter, 0, sizeof(unsigned), s));
   GW_HIP_TRY(hipMemsetAsync(t.error_flag, 0, sizeof(int), s));
   const int blocks = (int)std::min<int64_t>(t.blocks, nsrc);
-  hipError_t e = t.lds_row ? launch<true>(step, A, blocks, t.lds_bytes, s)
-                           : launch<false>(step, A, blocks, t.lds_bytes, s);
+  hipError_t e = t.lds_row == 0 ? launch<0>(step, A, blocks, t.lds_bytes, s)
+                                 : launch<1>(step, A, blocks, t.lds_bytes, s);
   if (e != hipSuccess) {
     g->err = std::string("k_topsim launch: ") + hipGetErrorString(e);
     return GW_ERR_DEVICE;
