@@ -123,6 +123,44 @@ __device__ __forceinline__ int upper_bound_i32(const int32_t* a, int n, int x) {
   return lo;
 }
 
+// wave 0 of the block: the radix bin holding the need-th key, scanning the
+// 256 bins from the top (desc) or from the bottom (asc); 4 bins per lane and
+// one wave scan instead of a serial 256-step loop.  Returns (bin, keys in
+// the bins scanned before it) through *bin / *before (lane 0 writes them).
+__device__ __forceinline__ void select_bin(const unsigned* hist, int need, bool desc, int* bin, int* before) {
+  const int lane = threadIdx.x & 63;
+  int c[4], loc = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int o = 4 * lane + q;
+    c[q] = (int)hist[desc ? 255 - o : o];
+    loc += c[q];
+  }
+  int inc = loc;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += t;
+  }
+  int run = inc - loc, first = -1, cum_at = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (first < 0 && run + c[q] >= need) {
+      first = 4 * lane + q;
+      cum_at = run;
+    }
+    run += c[q];
+  }
+  const unsigned long long m = __ballot(first >= 0);
+  const int src = m ? __ffsll(m) - 1 : 63;
+  const int o = __shfl(first >= 0 ? first : 255, src, 64);
+  const int cb = __shfl(first >= 0 ? cum_at : run - c[3], src, 64);
+  if (lane == 0) {
+    *bin = desc ? 255 - o : o;
+    *before = cb;
+  }
+}
+
 __device__ __forceinline__ unsigned long long dkey(double v) {
   return (unsigned long long)__double_as_longlong(v);  // v >= 0: bit order == value order
 }
@@ -139,7 +177,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
   __shared__ int s_wave[TS_WAVES + 1];
   __shared__ long long s_red[TS_WAVES];
   __shared__ int s_size[L + 2];
-  __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount;
+  __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount, s_bin, s_cum;
   __shared__ unsigned s_hist[256];
   __shared__ unsigned long long s_prefix, s_mask;
   __shared__ int32_t s_sel_id[TOPK_MAX];
@@ -538,14 +576,11 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
             if ((k & msk) == pre) atomicAdd(&s_hist[(k >> shift) & 255], 1u);
           }
           __syncthreads();
+          if (tid < 64) select_bin(s_hist, s_need, true, &s_bin, &s_cum);
+          __syncthreads();
           if (tid == 0) {
-            int need = s_need, cum = 0, b = 255;
-            for (; b > 0; --b) {
-              if (cum + (int)s_hist[b] >= need) break;
-              cum += s_hist[b];
-            }
-            s_need = need - cum;
-            s_prefix = pre | ((unsigned long long)b << shift);
+            s_need = s_need - s_cum;
+            s_prefix = pre | ((unsigned long long)s_bin << shift);
             s_mask = msk | (255ull << shift);
           }
           __syncthreads();
@@ -577,14 +612,11 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
               if ((k & msk) == pre) atomicAdd(&s_hist[(k >> shift) & 255], 1u);
             }
             __syncthreads();
+            if (tid < 64) select_bin(s_hist, s_need, false, &s_bin, &s_cum);
+            __syncthreads();
             if (tid == 0) {
-              int need = s_need, cum = 0, b = 0;
-              for (; b < 255; ++b) {
-                if (cum + (int)s_hist[b] >= need) break;
-                cum += s_hist[b];
-              }
-              s_need = need - cum;
-              s_prefix = pre | ((unsigned long long)b << shift);
+              s_need = s_need - s_cum;
+              s_prefix = pre | ((unsigned long long)s_bin << shift);
               s_mask = msk | (255ull << shift);
             }
             __syncthreads();
