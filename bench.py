@@ -25,7 +25,9 @@ Also reported (same JSON line):
   secondary     TopSim_singleSample on lshrank blog (STEP=5, SAMPLE=10000,
                 C=0.6, top-20, all 10,313 sources): pair-updates/s; and
                 secondary.simrank_naive: SimRank.java (STEP=3, C=0.6) on blog,
-                dense 10,313^2 fp64 result: rounds/s, LDS-gather roofline.
+                dense 10,313^2 fp64 result: rounds/s, LDS-gather roofline;
+                secondary.walk_10m: the north_star's 10M-node/100M-edge graph
+                (R-MAT scale 24, ef 6), 1 walk per node, with its CPU sample.
 """
 import argparse
 import json
@@ -61,6 +63,10 @@ def parse():
                     help="second-order sampler (auto: bitset when it fits in HBM)")
     ap.add_argument("--no-topsim", action="store_true")
     ap.add_argument("--no-simrank", action="store_true")
+    ap.add_argument("--no-walk10m", action="store_true",
+                    help="skip the north_star 10M-node/100M-edge walk measurement")
+    ap.add_argument("--walk10m-scale", type=int, default=24)
+    ap.add_argument("--walk10m-edge-factor", type=int, default=6)
     ap.add_argument("--simrank-graph", default="blog", help="naive SimRank graph (blog or moreno)")
     ap.add_argument("--simrank-rounds", type=int, default=3, help="SimRank.java STEP")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -416,6 +422,91 @@ def main():
                          "frac": gathers / sec / lds_peak, "traffic": None, "kernel": "k_sr_gather<true,*>"},
             "cpu_baseline": cpu_sr,
         }
+
+    # ---- north_star: walks on a ~10M-node / ~100M-edge power-law graph ----
+    def run_walk10m():
+        t0 = time.perf_counter()
+        BG = gwamd.GWGraph.rmat(args.walk10m_scale, args.walk10m_edge_factor, 0.57, 0.19, 0.19, args.seed + 1)
+        bi = BG.info()
+        build_s = time.perf_counter() - t0
+        BG.to_device(dev.index)
+        t0 = time.perf_counter()
+        bmode = "bitset"
+        try:
+            C.check(C.lib().gw_n2v_prepare(BG.handle, args.p, args.q, C.N2V_BITSET), BG.handle)
+        except C.CapacityError:
+            bmode = "rejection"
+            C.check(C.lib().gw_n2v_prepare(BG.handle, args.p, args.q, C.N2V_REJECTION), BG.handle)
+        torch.cuda.synchronize()
+        bprep = time.perf_counter() - t0
+        nb = int(bi.n)
+        bout = torch.empty((nb, L), dtype=torch.int32, device=dev)
+        bcnt = torch.zeros(2, dtype=torch.int64, device=dev)
+
+        def bstep(i):
+            w0 = gdist.weak_block(i, world, rank, nb)
+            C.check(C.lib().gw_n2v_walks(BG.handle, L, args.seed, w0, nb, 1, C.ptr(bout), None, C.ptr(bcnt), sh),
+                    BG.handle)
+        bstep(0)
+        torch.cuda.synchronize()
+        bcnt.zero_()
+        if world > 1:
+            dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t1 = time.perf_counter()
+        e0.record(stream)
+        bstep(1)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        sec = time.perf_counter() - t1
+        bsteps = int(bcnt[0].item())
+        if world > 1:
+            tt = torch.tensor([sec], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            sec = float(tt.item())
+            ss = torch.tensor([bsteps], dtype=torch.int64, device=dev)
+            dist.all_reduce(ss, op=dist.ReduceOp.SUM)
+            bsteps = int(ss.item())
+        kms = e0.elapsed_time(e1)
+        cpu_b = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            import oracle
+            csr_b = BG.export_csr()
+            nth = min(16, os.cpu_count() or 1)
+            fn = oracle.walks_bitset if bmode == "bitset" else (
+                lambda c, *a, **k: oracle.walks_scale(dict(c, weights=None), *a, **k))
+            nw = 2000
+            t2 = time.perf_counter()
+            fn(csr_b, args.p, args.q, args.seed, L, 0, nw, nthreads=nth)
+            dt = time.perf_counter() - t2
+            if dt < 5.0:  # grow the sample to ~10 s of CPU work
+                nw = int(nw * min(1000.0, 10.0 / max(dt, 1e-3)))
+                t2 = time.perf_counter()
+                fn(csr_b, args.p, args.q, args.seed, L, 0, nw, nthreads=nth)
+                dt = time.perf_counter() - t2
+            cpu_b = {"value": nw * (L - 1) / dt, "unit": "walk-steps/s", "cores": nth, "kind": "port",
+                     "sample": f"{nw} walks of the same graph and sampler ({bmode}), oracle/oracle.c, {dt:.1f} s",
+                     "reference_python_context": "the reference node2vec.py cannot build per-edge alias tables "
+                                                 "for this graph (sum(deg^2) entries); SURVEY §6 measured "
+                                                 "4.1e4-3.7e5 walk-steps/s/core on small graphs"}
+        del bout
+        BG.free()
+        return {"metric": "walk-steps/sec (node2vec, north_star 10M/100M graph)", "value": bsteps / sec,
+                "unit": "walk-steps/s",
+                "config": {"workload": f"node2vec p={args.p} q={args.q} on Graph500 R-MAT scale-{args.walk10m_scale} "
+                                       f"ef {args.walk10m_edge_factor} (n={bi.n}, adjacency entries={bi.nnz}), "
+                                       f"walk_length={L}, 1 walk/node per rank",
+                           "sampler": bmode},
+                "kernel_ms": kms, "host_build_s": build_s, "prepare_s": bprep, "cpu_baseline": cpu_b}
+
+    if not args.no_walk10m:
+        wb = run_walk10m()
+        if secondary is None:
+            secondary = {"walk_10m": wb}
+        else:
+            secondary["walk_10m"] = wb
 
     if not args.no_simrank:
         sr = run_simrank(args.simrank_graph)
