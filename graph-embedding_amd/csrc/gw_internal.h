@@ -49,6 +49,11 @@ GW_HD inline bool gw_bs_is_ef(uint32_t c, uint32_t d) {
 }
 static_assert(sizeof(gw_bs_nbr) == 64, "bitset entry must be one 64 B sector");
 
+struct gw_ts_ent {  // adjacency slot (u -> x): everything a walker's next step needs
+  int32_t x, d;      // neighbour, deg(x)
+  int64_t off;       // offsets[x]
+};
+
 struct gw_dev_graph {
   int64_t n = 0, nnz = 0;
   int64_t* offsets = nullptr;
@@ -65,12 +70,10 @@ struct gw_dev_graph {
   uint32_t* bitmap = nullptr;  // has_edge pre-filter, 16 bits per entry
   uint32_t* bs_region = nullptr;  // GW_N2V_BITSET per-edge regions (gw_n2v_bitset.hip)
   gw_bs_nbr* bs_nbr = nullptr;    // [nnz] neighbour + region offset
+  gw_ts_ent* sent = nullptr;      // [nnz] REJECTION mode: {x, deg(x), offsets[x]} per slot
 };
 
-struct gw_ts_ent {  // TopSim adjacency slot (u -> x): everything a walker's next step needs
-  int32_t x, d;      // neighbour, deg(x)
-  int64_t off;       // offsets[x]
-};
+
 
 struct gw_topsim_ws {
   int variant = -1, sample = 0, step = 0, topk = 0;
