@@ -85,7 +85,7 @@ def build(force=False, verbose=False):
     os.makedirs(bindir, exist_ok=True)
     hsrc = [os.path.join(host, "topsim_host.cpp")]
     hhdr = [os.path.join(host, "topsim_host.hpp"), os.path.join(ROOT, "include", "graphwalk.h")]
-    for drv in ["test_u_u_topsim_singlesample"]:
+    for drv in ["test_u_u_topsim_singlesample", "simrank_variants"]:
         exe = os.path.join(bindir, drv)
         dsrc = os.path.join(host, drv + ".cpp")
         if force or _newer(exe, hsrc + hhdr + [dsrc, OUT, __file__]):

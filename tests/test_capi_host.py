@@ -211,3 +211,24 @@ def test_select_fixed_max_pq_for_topsim_dev(gw, oracle):
     for i in range(30):
         exp = [j for j, _ in oracle.java_fixed_max_pq_row(cand[i], 7, min_score=topsim.MIN)]
         assert ids[i].tolist() == exp + [-1] * (7 - len(exp))
+
+
+def test_cachemap_writer_format(gw, oracle, tmp_path):
+    """Print.printByOrder(FixedCacheMap[], outPath, topk) (Print.java:94-124):
+    the last topk entries of each ascending iteration, %.6f of the float
+    value widened to double, CRLF; rows of fewer than topk print whole."""
+    from gwamd import _lib as C
+    cap = 6
+    keys = np.array([[5, 2, 9, 1, -1, -1], [3, 4, 7, 8, 0, 6], [-1] * 6], np.int32)
+    vals = np.array([[0.1, 0.25, 0.3, 1.5, 0, 0], [1e-7, 2e-7, 0.5, 0.5, 0.75, 3.0], [0] * 6], np.float32)
+    size = np.array([4, 6, 0], np.int32)
+    out = tmp_path / "c.txt"
+    C.check(C.lib().gw_write_sim_text_cachemap(str(out).encode(), C.ptr(keys), C.ptr(vals), C.ptr(size), None, 3,
+                                               cap, 4, b","))
+    lines = open(str(out) + ".sim.txt", "rb").read().split(b"\r\n")
+    ids = open(out, "rb").read().split(b"\r\n")
+    for r in range(3):
+        lo = max(0, size[r] - 4)
+        exp = [(int(keys[r, i]), float(vals[r, i])) for i in range(lo, size[r])]
+        assert lines[r].decode() == f"{r}" + "".join(f",{k}:{oracle.java_format_fixed(v)}" for k, v in exp)
+        assert ids[r].decode() == f"{r}" + "".join(f",{k}" for k, _ in exp)

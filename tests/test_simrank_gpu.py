@@ -136,3 +136,50 @@ def test_print_by_order_all(gw, oracle, tmp_path):
     for v in (0, 1, 100, 332):
         exp = oracle.java_fixed_max_pq_row(sim[v], 1000)
         assert lines[v].decode() == f"{v}" + "".join(f" {i}:{oracle.java_format_fixed(x, 7)}" for i, x in exp)
+
+
+def test_cpp_variants_driver_matches_python(gw, tmp_path):
+    """The C++ host mirror (host/simrank_variants.cpp over topsim_host.hpp)
+    produces the same files / matrices as the Python mirror for SimRank,
+    TopSim_singleSample_M, SingleRandomWalk_M, TopSim_doubleSample, TopSim_Dev
+    and DoubleRandomWalk (same library, same seeds)."""
+    import subprocess
+    from conftest import ROOT
+    from gwamd import topsim
+    exe = os.path.join(ROOT, "graph-embedding_amd", "bin", "simrank_variants")
+    f, V, sep = GRAPHS["g333"]
+    path = os.path.join(DATA, f)
+
+    def run(algo, *extra):
+        out = str(tmp_path / algo)
+        subprocess.run([exe, "--graph", path, "--V", str(V), "--sep", sep, "--algo", algo, "--out", out,
+                        "--seed", "3", *extra], check=True, timeout=600)
+        return out
+
+    g = _graph("g333")
+    # SimRank.main: printByOrderAll(sim, out, 1000, 10) with MyConfiguration.SEPARATOR
+    out = run("simrank", "--step", "3")
+    sr = topsim.SimRank(g)
+    sr.compute()
+    topsim.printByOrderAll(sr, str(tmp_path / "py_sr"), 1000, 10, separator=sep)
+    assert open(out + ".sim.txt", "rb").read() == open(str(tmp_path / "py_sr") + ".sim.txt", "rb").read()
+    for algo, cls in (("topsim_m", topsim.TopSim_singleSample_M), ("srw_m", topsim.SingleRandomWalk_M)):
+        out = run(algo, "--M", "2", "--sample", "500", "--step", "3")
+        ts = cls(g, 2, 500, seed=3, step=3)
+        ts.compute()
+        topsim.printByOrder(ts, str(tmp_path / ("py_" + algo)), 20, separator=sep)
+        assert open(out + ".sim.txt", "rb").read() == open(str(tmp_path / ("py_" + algo)) + ".sim.txt", "rb").read()
+    out = run("double", "--sample", "100", "--step", "3")
+    ds = topsim.TopSim_doubleSample(g, 100, 3, seed=3)
+    ds.compute()
+    assert np.array_equal(np.fromfile(out + ".bin").reshape(V, V), ds.getResult())
+    out = run("drw", "--sample", "10", "--step", "3")
+    dw = topsim.DoubleRandomWalk(g, 10, 3, seed=3)
+    dw.compute()
+    np.testing.assert_allclose(np.fromfile(out + ".bin").reshape(V, V), dw.getResult(), rtol=1e-12, atol=1e-15)
+    out = run("dev", "--sample", "3000", "--step", "3", "--topk", "5", "--single", "1")
+    dev = topsim.TopSim_Dev(g, 3000, 3, 5, 1, seed=3)
+    sr2 = topsim.SimRank(g)
+    sr2.compute()
+    dev.compute(sr2.getResult())
+    np.testing.assert_allclose(np.fromfile(out + ".bin").reshape(V, V), dev.getResult(), rtol=1e-12, atol=1e-15)
