@@ -30,6 +30,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 
 #include "gw_device_common.h"
 
@@ -71,6 +73,7 @@ struct TsArgs {
   int32_t* touched;
   unsigned int* src_counter;
   int* error_flag;
+  unsigned long long* phase;  // diagnostics (GW_DIAG_TS_PHASES): cycles per phase, thread 0 of each block
 };
 
 __device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int* total) {
@@ -177,7 +180,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
   __shared__ int s_wave[TS_WAVES + 1];
   __shared__ long long s_red[TS_WAVES];
   __shared__ int s_size[L + 2];
-  __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount, s_bin, s_cum;
+  __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount, s_bin, s_cum, s_exact;
   __shared__ unsigned s_hist[256];
   __shared__ unsigned long long s_prefix, s_mask;
   __shared__ int32_t s_sel_id[TOPK_MAX];
@@ -291,7 +294,16 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
     ++my_upd;
   };
 
+  unsigned long long ph_t = 0, ph[5] = {0, 0, 0, 0, 0};
+  auto mark = [&](int k) {  // diagnostics only
+    if (A.phase && tid == 0) {
+      const unsigned long long now = __builtin_readcyclecounter();
+      if (k >= 0) ph[k] += now - ph_t;
+      ph_t = now;
+    }
+  };
   for (;;) {
+    mark(-1);
     if (tid == 0) {
       s_src = (int)atomicAdd(A.src_counter, 1u);
       s_abort = 0;
@@ -426,6 +438,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
         }
         __syncthreads();
       }
+      mark(0);
       // walker index prefix over spawners (queue order)
       const int ns = s_abort ? 0 : s_nspawn;
       int run = 0;
@@ -445,6 +458,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
       __syncthreads();
     }
 
+    mark(1);
     // random walkers: one lane each, path in registers
     {
       const int W = s_nwalk;
@@ -493,6 +507,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
     }
     __syncthreads();
 
+    mark(2);
     // ---- output ------------------------------------------------------------
     // hash mode: fold overflow entries whose key also reached the LDS table
     // (a key can straddle the load limit) into the LDS entry
@@ -557,11 +572,14 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
       unsigned long long T = 0;  // threshold key (K-th largest)
       int32_t idT = 0x7fffffff;  // largest id taken at key == T
       bool take_all = (C <= K);
+      bool bin_exact = false;    // the K-th key's bin is taken whole: select by masked prefix
+      unsigned long long Tmask = ~0ull;
       if (!take_all) {
         if (tid == 0) {
           s_prefix = 0;
           s_mask = 0;
           s_need = K;
+          s_exact = 0;
         }
         __syncthreads();
         for (int shift = 56; shift >= 0; shift -= 8) {
@@ -579,13 +597,21 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
           if (tid < 64) select_bin(s_hist, s_need, true, &s_bin, &s_cum);
           __syncthreads();
           if (tid == 0) {
-            s_need = s_need - s_cum;
+            const int rest = s_need - s_cum;
+            // the chosen bin holds exactly the keys still needed: all of it is taken
+            if ((int)s_hist[s_bin] == rest) s_exact = 1;
+            s_need = rest;
             s_prefix = pre | ((unsigned long long)s_bin << shift);
             s_mask = msk | (255ull << shift);
           }
           __syncthreads();
+          if (s_exact) break;
         }
+        bin_exact = s_exact != 0;
+        Tmask = s_mask;
         T = s_prefix;
+      }
+      if (!take_all && !bin_exact) {
         // ties at the threshold: smallest ids first
         long long eq_local = 0;
         for (int idx = tid; idx < NC; idx += TS_BLOCK) {
@@ -631,7 +657,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
         double v;
         if (!cand(idx, &id, &v)) continue;
         const unsigned long long k = dkey(v);
-        if (take_all || k > T || (k == T && id <= idT)) {
+        if (take_all || (bin_exact ? (k & Tmask) >= T : (k > T || (k == T && id <= idT)))) {
           int slot = atomicAdd(&s_cnt, 1);
           if (slot < TOPK_MAX) {
             s_sel_id[slot] = id;
@@ -678,6 +704,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
       }
     }
     __syncthreads();
+    mark(3);
     // re-zero the accumulator for the next source
     if (LDS_ROW) {
       for (int t = tid; t < n; t += TS_BLOCK) s_row[t] = 0.0;
@@ -698,8 +725,11 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
       s_hcount = 0;
     }
     __syncthreads();
+    mark(4);
   }
 
+  if (A.phase && tid == 0)
+    for (int k = 0; k < 5; ++k) atomicAdd(&A.phase[k], ph[k]);
   // statistics
   long long e = block_sum<long long>(my_ext, s_red);
   long long u = block_sum<long long>(my_upd, s_red);
@@ -932,6 +962,13 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   GW_HIP_TRY(hipMemsetAsync(t.src_counter, 0, sizeof(unsigned), s));
   GW_HIP_TRY(hipMemsetAsync(t.error_flag, 0, sizeof(int), s));
   const int blocks = (int)std::min<int64_t>(t.blocks, nsrc);
+  // GW_DIAG_TS_PHASES=1: cycles per kernel phase summed over blocks, to stderr (diagnostics only)
+  const char* dph = std::getenv("GW_DIAG_TS_PHASES");
+  A.phase = nullptr;
+  if (dph && dph[0] == '1') {
+    GW_HIP_TRY(hipMalloc((void**)&A.phase, 5 * sizeof(unsigned long long)));
+    GW_HIP_TRY(hipMemsetAsync(A.phase, 0, 5 * sizeof(unsigned long long), s));
+  }
   hipError_t e = t.lds_row == 0 ? launch<0>(step, A, blocks, t.lds_bytes, s)
                                  : launch<1>(step, A, blocks, t.lds_bytes, s);
   if (e != hipSuccess) {
@@ -941,6 +978,13 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   int flag = 0;
   GW_HIP_TRY(hipMemcpyAsync(&flag, t.error_flag, sizeof(int), hipMemcpyDeviceToHost, s));
   GW_HIP_TRY(hipStreamSynchronize(s));
+  if (A.phase) {
+    unsigned long long ph[5];
+    GW_HIP_TRY(hipMemcpy(ph, A.phase, sizeof ph, hipMemcpyDeviceToHost));
+    (void)hipFree(A.phase);
+    std::fprintf(stderr, "[k_topsim phases, cycles summed over %d blocks] levels %llu walkers %llu output %llu "
+                 "clear %llu (spawn-prefix %llu)\n", blocks, ph[0] + 0ull, ph[2], ph[3], ph[4], ph[1]);
+  }
   if (flag) {
     g->err = "TopSim frontier exceeded the workspace (level/spawn/touch capacity)";
     return GW_ERR_CAPACITY;
