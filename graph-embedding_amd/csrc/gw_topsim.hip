@@ -666,41 +666,35 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
         }
       }
       __syncthreads();
-      const int cnt = min(s_cnt, K);
-      // pad to a power of two and bitonic-sort by (value desc, id asc)
-      int P2 = 1;
-      while (P2 < cnt) P2 <<= 1;
-      for (int i = cnt + tid; i < P2; i += TS_BLOCK) {
-        s_sel_id[i] = 0x7fffffff;
-        s_sel_val[i] = -1.0;
-      }
-      __syncthreads();
-      for (int size = 2; size <= P2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-          for (int i = tid; i < P2; i += TS_BLOCK) {
-            const int jx = i ^ stride;
-            if (jx > i) {
-              const bool up = ((i & size) == 0);
-              const double vi = s_sel_val[i], vj = s_sel_val[jx];
-              const int32_t ii = s_sel_id[i], ij = s_sel_id[jx];
-              // "i before j" in final order: larger value, then smaller id
-              const bool i_first = (vi > vj) || (vi == vj && ii < ij);
-              if (i_first != up) {
-                s_sel_val[i] = vj;
-                s_sel_val[jx] = vi;
-                s_sel_id[i] = ij;
-                s_sel_id[jx] = ii;
-              }
-            }
-          }
-          __syncthreads();
-        }
-      }
+      const int cnt = min(s_cnt, TOPK_MAX);
+      // order by (value desc, id asc): every selected entry counts the entries
+      // that precede it (<= 256 entries, one pass, broadcast LDS reads)
       int32_t* oid = A.out_ids + r * (int64_t)K;
       double* osc = A.out_scores + r * (int64_t)K;
-      for (int k = tid; k < K; k += TS_BLOCK) {
-        oid[k] = k < cnt ? s_sel_id[k] : -1;
-        osc[k] = k < cnt ? s_sel_val[k] : 0.0;
+      {
+        // G threads per entry (cnt <= 128: 4, else 2), partial counts summed with lane shuffles
+        const int G = cnt <= TS_BLOCK / 4 ? 4 : 2;
+        const int i = tid / G, sub = tid % G;
+        int rank = 0;
+        double vi = 0.0;
+        int32_t ii = 0;
+        if (i < cnt) {
+          vi = s_sel_val[i];
+          ii = s_sel_id[i];
+          for (int j = sub; j < cnt; j += G) {
+            const double vj = s_sel_val[j];
+            rank += (vj > vi) || (vj == vi && s_sel_id[j] < ii);
+          }
+        }
+        for (int o = 1; o < G; o <<= 1) rank += __shfl_xor(rank, o, 64);
+        if (i < cnt && sub == 0 && rank < K) {
+          oid[rank] = ii;
+          osc[rank] = vi;
+        }
+      }
+      for (int k = min(cnt, K) + tid; k < K; k += TS_BLOCK) {
+        oid[k] = -1;
+        osc[k] = 0.0;
       }
     }
     __syncthreads();
