@@ -193,8 +193,8 @@ def main():
     log(f"[rank {rank}] rmat-{args.scale}: n={n} nnz={nnz} maxdeg={inf.max_degree} "
         f"built in {time.perf_counter() - t0:.1f}s")
     G.to_device(dev.index)
-    # sampler: per-edge common-neighbour bitsets when sum(deg^2) bits fit in
-    # HBM (exact 3-way mixture, ~2 lines per step), else rejection sampling
+    # sampler: per-edge 64 B entries + common-neighbour regions when they fit
+    # in HBM (exact 3-way mixture, ~1.5 lines per step), else rejection sampling
     t0 = time.perf_counter()
     mode = "bitset" if args.mode in ("auto", "bitset") else "rejection"
     if mode == "bitset":
@@ -209,7 +209,8 @@ def main():
         C.check(C.lib().gw_n2v_prepare(G.handle, args.p, args.q, C.N2V_REJECTION), G.handle)
     torch.cuda.synchronize()
     prep_s = time.perf_counter() - t0
-    log(f"[rank {rank}] prepare ({mode}) {prep_s:.2f}s")
+    sampler_gb = G.info().sampler_bytes / 1e9
+    log(f"[rank {rank}] prepare ({mode}) {prep_s:.2f}s, sampler tables {sampler_gb:.2f} GB")
 
     B = args.num_walks * n                      # walks per rank per step
     out = torch.empty((B, L), dtype=torch.int32, device=dev)
@@ -424,21 +425,20 @@ def main():
         }
 
     # ---- north_star: walks on a ~10M-node / ~100M-edge power-law graph ----
-    def run_walk10m():
-        t0 = time.perf_counter()
-        BG = gwamd.GWGraph.rmat(args.walk10m_scale, args.walk10m_edge_factor, 0.57, 0.19, 0.19, args.seed + 1)
+    def run_walk10m(BG, build_s, wp, wq):
         bi = BG.info()
-        build_s = time.perf_counter() - t0
-        BG.to_device(dev.index)
         t0 = time.perf_counter()
         bmode = "bitset"
         try:
-            C.check(C.lib().gw_n2v_prepare(BG.handle, args.p, args.q, C.N2V_BITSET), BG.handle)
+            C.check(C.lib().gw_n2v_prepare(BG.handle, wp, wq, C.N2V_BITSET), BG.handle)
         except C.CapacityError:
             bmode = "rejection"
-            C.check(C.lib().gw_n2v_prepare(BG.handle, args.p, args.q, C.N2V_REJECTION), BG.handle)
+            C.check(C.lib().gw_n2v_prepare(BG.handle, wp, wq, C.N2V_REJECTION), BG.handle)
         torch.cuda.synchronize()
+        if wp == 1.0 and wq == 1.0:
+            bmode = "first-order"  # k_walk_scale<true,...>: no per-edge tables
         bprep = time.perf_counter() - t0
+        bsampler_gb = BG.info().sampler_bytes / 1e9
         nb = int(bi.n)
         bout = torch.empty((nb, L), dtype=torch.int32, device=dev)
         bcnt = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -475,38 +475,45 @@ def main():
             import oracle
             csr_b = BG.export_csr()
             nth = min(16, os.cpu_count() or 1)
-            fn = oracle.walks_bitset if bmode == "bitset" else (
-                lambda c, *a, **k: oracle.walks_scale(dict(c, weights=None), *a, **k))
+            # the CPU restatement of the rejection sampler (same walk distribution): the oracle's
+            # bitset restatement rebuilds each bitset per step and is no fair CPU baseline
+            fn = lambda c, *a, **k: oracle.walks_scale(dict(c, weights=None), *a, **k)  # noqa: E731
             nw = 2000
             t2 = time.perf_counter()
-            fn(csr_b, args.p, args.q, args.seed, L, 0, nw, nthreads=nth)
+            fn(csr_b, wp, wq, args.seed, L, 0, nw, nthreads=nth)
             dt = time.perf_counter() - t2
-            if dt < 5.0:  # grow the sample to ~10 s of CPU work
+            if dt < 5.0:  # grow the sample to ~10 s of CPU work (first-order walks are cheap: cap it)
                 nw = int(nw * min(1000.0, 10.0 / max(dt, 1e-3)))
                 t2 = time.perf_counter()
-                fn(csr_b, args.p, args.q, args.seed, L, 0, nw, nthreads=nth)
+                fn(csr_b, wp, wq, args.seed, L, 0, nw, nthreads=nth)
                 dt = time.perf_counter() - t2
             cpu_b = {"value": nw * (L - 1) / dt, "unit": "walk-steps/s", "cores": nth, "kind": "port",
-                     "sample": f"{nw} walks of the same graph and sampler ({bmode}), oracle/oracle.c, {dt:.1f} s",
+                     "sample": f"{nw} walks of the same graph, p and q, oracle/oracle.c or_walks_scale "
+                               f"(rejection sampler), {dt:.1f} s",
                      "reference_python_context": "the reference node2vec.py cannot build per-edge alias tables "
                                                  "for this graph (sum(deg^2) entries); SURVEY §6 measured "
                                                  "4.1e4-3.7e5 walk-steps/s/core on small graphs"}
         del bout
-        BG.free()
         return {"metric": "walk-steps/sec (node2vec, north_star 10M/100M graph)", "value": bsteps / sec,
                 "unit": "walk-steps/s",
-                "config": {"workload": f"node2vec p={args.p} q={args.q} on Graph500 R-MAT scale-{args.walk10m_scale} "
+                "config": {"workload": f"node2vec p={wp} q={wq} on Graph500 R-MAT scale-{args.walk10m_scale} "
                                        f"ef {args.walk10m_edge_factor} (n={bi.n}, adjacency entries={bi.nnz}), "
                                        f"walk_length={L}, 1 walk/node per rank",
                            "sampler": bmode},
-                "kernel_ms": kms, "host_build_s": build_s, "prepare_s": bprep, "cpu_baseline": cpu_b}
+                "kernel_ms": kms, "host_build_s": build_s, "prepare_s": bprep, "sampler_tables_gb": bsampler_gb,
+                "cpu_baseline": cpu_b}
 
     if not args.no_walk10m:
-        wb = run_walk10m()
+        t0 = time.perf_counter()
+        BG = gwamd.GWGraph.rmat(args.walk10m_scale, args.walk10m_edge_factor, 0.57, 0.19, 0.19, args.seed + 1)
+        build_s = time.perf_counter() - t0
+        BG.to_device(dev.index)
         if secondary is None:
-            secondary = {"walk_10m": wb}
-        else:
-            secondary["walk_10m"] = wb
+            secondary = {}
+        # the bench's p/q, then p=q=1 (the north_star graph walked first-order)
+        secondary["walk_10m"] = run_walk10m(BG, build_s, args.p, args.q)
+        secondary["walk_10m_p1q1"] = run_walk10m(BG, build_s, 1.0, 1.0)
+        BG.free()
 
     if not args.no_simrank:
         sr = run_simrank(args.simrank_graph)
@@ -540,7 +547,7 @@ def main():
                        "global_batch": B * world, "seq_len": L, "parallelism": f"dp{world}",
                        "allgather": bool(gather is not None)},
             "walk_steps": steps_total,
-            "sampler": mode, "prepare_seconds": prep_s,
+            "sampler": mode, "prepare_seconds": prep_s, "sampler_tables_gb": sampler_gb,
             "rejection_trials_per_step": trials_total / max(steps_total, 1),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -87,22 +87,217 @@ __device__ __forceinline__ int word_select(uint32_t x, uint32_t j) {
   return pos;
 }
 
-__global__ void k_bs_sizes(int64_t nnz, const int32_t* __restrict__ nbrs, const int32_t* __restrict__ deg,
-                           uint64_t* __restrict__ sz) {
-  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= nnz) return;
-  sz[e] = (uint64_t)bs_words(deg[nbrs[e]]);
+// ---- build ------------------------------------------------------------------
+// Common neighbours of slot (u -> v) are enumerated from the SHORTER of the two
+// sorted rows: over N(v) with has_edge(u, x) probes, or over N(u) with a
+// search in N(v) (the search window only moves forward, rows being sorted).
+// Either way positions k in N(v) come out ascending, so cost is
+// min(deg u, deg v) probes per slot instead of deg(v).
+constexpr int kThreadMin = 64;  // slots whose shorter row is <= this: one thread, else one wave
+
+enum { BS_LIST = 0, BS_INLINE = 1, BS_EF = 2, BS_REGION = 3 };
+__device__ __forceinline__ int bs_mode(uint32_t c, uint32_t d) {
+  return gw_bs_is_list(c, d) ? BS_LIST : d <= (uint32_t)GW_BS_INLINE_BITS ? BS_INLINE : gw_bs_is_ef(c, d) ? BS_EF : BS_REGION;
 }
 
-// thread per slot for small deg(v); larger slots are queued for the wave kernel
-__global__ void k_bs_fill_small(gw_dev_graph G, const uint64_t* __restrict__ roff, uint32_t* __restrict__ reg,
-                                gw_bs_nbr* __restrict__ bsn, int64_t* __restrict__ big,
-                                unsigned long long* __restrict__ nbig) {
+// first index in [b, e) with nbrs[i] >= key
+__device__ __forceinline__ int64_t lower_bound_i32(const int32_t* __restrict__ a, int64_t b, int64_t e, int32_t key) {
+  while (b < e) {
+    const int64_t mid = (b + e) >> 1;
+    if (a[mid] < key)
+      b = mid + 1;
+    else
+      e = mid;
+  }
+  return b;
+}
+
+struct BsSlot {
+  int32_t u;
+  int64_t ub, ue, vb, ve;
+};
+
+__device__ __forceinline__ BsSlot bs_slot(const gw_dev_graph& G, int64_t e) {
+  BsSlot S;
+  const int32_t v = G.nbrs[e];
+  S.u = row_of_slot(G.offsets, G.n, e);
+  S.ub = G.offsets[S.u];
+  S.ue = G.offsets[S.u + 1];
+  S.vb = G.offsets[v];
+  S.ve = G.offsets[v + 1];
+  return S;
+}
+
+// one thread: f(k, idx, kprev) per common position k (ascending), idx its rank
+template <class F>
+__device__ uint32_t common_thread(const gw_dev_graph& G, const BsSlot& S, F&& f) {
+  uint32_t c = 0;
+  int64_t kprev = -1;
+  if (S.ve - S.vb <= S.ue - S.ub) {
+    for (int64_t k = 0; k < S.ve - S.vb; ++k) {
+      const int32_t x = G.nbrs[S.vb + k];
+      if (x != S.u && bs_has_edge(G, S.ub, S.ue, x)) {
+        f(k, c++, kprev);
+        kprev = k;
+      }
+    }
+  } else {
+    int64_t lo = S.vb;
+    for (int64_t j = S.ub; j < S.ue && lo < S.ve; ++j) {
+      const int32_t x = G.nbrs[j];
+      if (x == S.u) continue;
+      lo = lower_bound_i32(G.nbrs, lo, S.ve, x);
+      if (lo < S.ve && G.nbrs[lo] == x) {
+        f(lo - S.vb, c++, kprev);
+        kprev = lo - S.vb;
+      }
+    }
+  }
+  return c;
+}
+
+// one wave: 64 probes per round; lanes holding a common position call f with
+// its rank and the previous common position (-1 for the first)
+template <class F>
+__device__ uint32_t common_wave(const gw_dev_graph& G, const BsSlot& S, F&& f, int64_t* klast) {
+  const int lane = threadIdx.x & 63;
+  const bool vside = S.ve - S.vb <= S.ue - S.ub;
+  const int64_t len = vside ? S.ve - S.vb : S.ue - S.ub;
+  uint32_t c = 0;
+  int carry = -1;
+  for (int64_t base = 0; base < len; base += 64) {
+    const int64_t j = base + lane;
+    bool found = false;
+    int k = 0;
+    if (j < len) {
+      if (vside) {
+        const int32_t x = G.nbrs[S.vb + j];
+        k = (int)j;
+        found = x != S.u && bs_has_edge(G, S.ub, S.ue, x);
+      } else {
+        const int32_t x = G.nbrs[S.ub + j];
+        if (x != S.u) {
+          const int64_t p = gw_row_find(G.nbrs, S.vb, S.ve, x);
+          if (p >= 0) {
+            found = true;
+            k = (int)(p - S.vb);
+          }
+        }
+      }
+    }
+    const unsigned long long m = __ballot(found);
+    if (!m) continue;
+    const unsigned long long lt = m & ((1ull << lane) - 1ull);
+    const int kp_in = __shfl(k, lt ? 63 - __clzll(lt) : 0, 64);
+    const int kl = __shfl(k, 63 - __clzll(m), 64);
+    if (found) f((int64_t)k, c + (uint32_t)__popcll(lt), (int64_t)(lt ? kp_in : carry));
+    c += (uint32_t)__popcll(m);
+    carry = kl;
+  }
+  *klast = carry;
+  return c;
+}
+
+// payload writer for one common position (entry words zeroed beforehand)
+struct BsEmit {
+  int mode;
+  uint32_t* w;     // entry payload
+  uint32_t* dir;   // region directory (ndir > 0)
+  uint32_t* bits;  // region bits
+  int64_t ndir;
+  int l;
+  uint32_t U;
+  __device__ void operator()(int64_t k, uint32_t idx, int64_t kprev) const {
+    const uint32_t bit = 1u << (k & 31);
+    if (mode == BS_LIST) {
+      reinterpret_cast<uint16_t*>(w)[idx] = (uint16_t)k;
+    } else if (mode == BS_INLINE) {
+      atomicOr(&w[k >> 5], bit);
+    } else if (mode == BS_EF) {
+      const uint32_t hp = (uint32_t)(k >> l) + idx;  // high part, unary
+      atomicOr(&w[hp >> 5], 1u << (hp & 31));
+      if (l > 0) {
+        const uint32_t lowv = (uint32_t)k & ((1u << l) - 1u), off = U + idx * (uint32_t)l, sh = off & 31;
+        atomicOr(&w[off >> 5], lowv << sh);
+        if (sh + (uint32_t)l > 32u) atomicOr(&w[(off >> 5) + 1], lowv >> (32 - sh));
+      }
+    } else {
+      atomicOr(&bits[k >> 5], bit);
+      if (ndir > 0)  // dir[g] = #positions below block g
+        for (int64_t g = (kprev < 0 ? -1 : kprev / kDirBits) + 1; g <= k / kDirBits; ++g) dir[g] = idx;
+    }
+  }
+};
+
+__device__ __forceinline__ BsEmit bs_emit(gw_bs_nbr* en, uint32_t* reg, const uint64_t* roff, int64_t e, uint32_t c,
+                                          uint32_t d) {
+  BsEmit E;
+  E.mode = bs_mode(c, d);
+  E.w = en->w;
+  E.ndir = 0;
+  E.dir = E.bits = nullptr;
+  E.l = 0;
+  E.U = 0;
+  if (E.mode == BS_EF) {
+    E.l = gw_bs_ef_l(c, d);
+    E.U = c + ((d - 1) >> E.l) + 1;
+  } else if (E.mode == BS_REGION) {
+    E.dir = reg + roff[e];
+    E.bits = E.dir + bs_boff(d);
+    E.ndir = bs_ndir(d);
+  }
+  return E;
+}
+
+// pass 1 (slots with deg(v) > kSmallD): entry header {x, d, offsets[x], kp, c};
+// slots whose shorter row exceeds kThreadMin are queued for the wave kernel
+__global__ void k_bs_count(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn, int64_t* __restrict__ big,
+                           unsigned long long* __restrict__ nbig) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= G.nnz) return;
+  const int32_t v = G.nbrs[e];
+  const int64_t vb = G.offsets[v], d = G.offsets[v + 1] - vb;
+  if (d <= kSmallD) return;  // k_bs_fill_small
+  const BsSlot S = bs_slot(G, e);
+  const int64_t kp = gw_row_find(G.nbrs, S.vb, S.ve, S.u);
+  uint32_t c = 0;
+  if (min(S.ue - S.ub, d) <= kThreadMin)
+    c = common_thread(G, S, [](int64_t, uint32_t, int64_t) {});
+  else
+    big[atomicAdd(nbig, 1ull)] = e;
+  gw_bs_nbr* en = bsn + e;
+  *reinterpret_cast<uint4*>(en) = make_uint4((uint32_t)v, (uint32_t)d, (uint32_t)(uint64_t)vb, (uint32_t)((uint64_t)vb >> 32));
+  *reinterpret_cast<uint2*>(&en->kp) = make_uint2(kp >= 0 ? (uint32_t)(kp - vb) : 0xFFFFFFFFu, c);
+}
+
+__global__ void k_bs_count_wave(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn, const int64_t* __restrict__ big,
+                                const unsigned long long* __restrict__ nbig) {
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t total = (int64_t)*nbig;
+  for (int64_t i = wave; i < total; i += nwaves) {
+    const int64_t e = big[i];
+    int64_t kl;
+    const uint32_t c = common_wave(G, bs_slot(G, e), [](int64_t, uint32_t, int64_t) {}, &kl);
+    if ((threadIdx.x & 63) == 0) bsn[e].c = c;
+  }
+}
+
+// region words per slot: only slots whose payload is neither list, inline nor Elias-Fano
+__global__ void k_bs_sizes(gw_dev_graph G, const gw_bs_nbr* __restrict__ bsn, uint64_t* __restrict__ sz) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= G.nnz) return;
+  const uint32_t d = (uint32_t)G.deg[G.nbrs[e]];
+  sz[e] = (d > (uint32_t)GW_BS_INLINE_BITS && bs_mode(bsn[e].c, d) == BS_REGION) ? (uint64_t)bs_words(d) : 0ull;
+}
+
+// deg(v) <= kSmallD: one thread builds the whole entry (list or inline bitset)
+__global__ void k_bs_fill_small(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn) {
   int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= G.nnz) return;
   const int32_t v = G.nbrs[e];
-  const uint64_t R = roff[e];
   const int64_t vb = G.offsets[v], d = G.offsets[v + 1] - vb;
+  if (d > kSmallD) return;
   gw_bs_nbr en;
   en.x = (uint32_t)v;
   en.kp = 0xFFFFFFFFu;
@@ -112,15 +307,6 @@ __global__ void k_bs_fill_small(gw_dev_graph G, const uint64_t* __restrict__ rof
   en.off_hi = (uint32_t)((uint64_t)vb >> 32);
 #pragma unroll
   for (int t = 0; t < 10; ++t) en.w[t] = 0;
-  if (d > GW_BS_INLINE_BITS) {
-    en.w[0] = (uint32_t)R;
-    en.w[1] = (uint32_t)(R >> 32);
-  }
-  if (d > kSmallD) {
-    bsn[e] = en;  // c, kp filled by k_bs_fill_wave
-    big[atomicAdd(nbig, 1ull)] = e;
-    return;
-  }
   const int32_t u = row_of_slot(G.offsets, G.n, e);
   const int64_t ub = G.offsets[u], ue = G.offsets[u + 1];
   uint32_t word = 0, c = 0;
@@ -145,7 +331,35 @@ __global__ void k_bs_fill_small(gw_dev_graph G, const uint64_t* __restrict__ rof
   bsn[e] = en;
 }
 
-// one wave per large slot: 64 neighbours per ballot
+// pass 2, one thread per slot (deg(v) > kSmallD, shorter row <= kThreadMin)
+__global__ void k_bs_fill_thread(gw_dev_graph G, const uint64_t* __restrict__ roff, uint32_t* __restrict__ reg,
+                                 gw_bs_nbr* __restrict__ bsn) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= G.nnz) return;
+  const int32_t v = G.nbrs[e];
+  const int64_t d = G.offsets[v + 1] - G.offsets[v];
+  if (d <= kSmallD) return;
+  const BsSlot S = bs_slot(G, e);
+  if (min(S.ue - S.ub, d) > kThreadMin) return;  // k_bs_fill_wave
+  gw_bs_nbr* en = bsn + e;
+  const uint32_t c = en->c;
+  const BsEmit E = bs_emit(en, reg, roff, e, c, (uint32_t)d);
+  if (E.mode == BS_LIST) {
+    for (uint32_t t = c; t < 2 * 10; ++t) reinterpret_cast<uint16_t*>(en->w)[t] = 0xFFFFu;
+  } else if (E.mode == BS_REGION) {
+    en->w[0] = (uint32_t)roff[e];
+    en->w[1] = (uint32_t)(roff[e] >> 32);
+  }
+  int64_t klast = -1;
+  common_thread(G, S, [&](int64_t k, uint32_t idx, int64_t kprev) {
+    E(k, idx, kprev);
+    klast = k;
+  });
+  if (E.mode == BS_REGION)
+    for (int64_t g = (klast < 0 ? -1 : klast / kDirBits) + 1; g < E.ndir; ++g) E.dir[g] = c;
+}
+
+// pass 2, one wave per queued slot
 __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff, uint32_t* __restrict__ reg,
                                gw_bs_nbr* __restrict__ bsn, const int64_t* __restrict__ big,
                                const unsigned long long* __restrict__ nbig) {
@@ -155,80 +369,15 @@ __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff
   const int64_t total = (int64_t)*nbig;
   for (int64_t i = wave; i < total; i += nwaves) {
     const int64_t e = big[i];
-    const int32_t v = G.nbrs[e];
-    const int32_t u = row_of_slot(G.offsets, G.n, e);
-    const int64_t vb = G.offsets[v], d = G.offsets[v + 1] - vb;
-    const int64_t ub = G.offsets[u], ue = G.offsets[u + 1];
-    const bool inl = d <= GW_BS_INLINE_BITS;
-    uint32_t* h = inl ? bsn[e].w : reg + roff[e];
-    const int64_t ndir = inl ? 0 : bs_ndir(d);
-    uint32_t* dir = h;
-    uint32_t* bits = h + bs_boff(d);
-    uint32_t c = 0;
-    int kp_local = -1;
-    int my_pos = 0xFFFF;  // lane t < GW_BS_LIST: position of the t-th common neighbour
-    for (int64_t base = 0; base < d; base += 64) {
-      const int64_t k = base + lane;
-      bool bit = false;
-      if (k < d) {
-        const int32_t x = G.nbrs[vb + k];
-        if (x == u)
-          kp_local = (int)k;
-        else
-          bit = bs_has_edge(G, ub, ue, x);
-      }
-      const unsigned long long m = __ballot(bit);
-      {
-        // lane t collects the t-th set bit overall when it falls in this ballot
-        const int pc = __popcll(m);
-        const int r = lane - (int)c;
-        int src = 0;
-        if (r >= 0 && r < pc) {
-          const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
-          const int plo = __popc(lo);
-          src = r < plo ? word_select(lo, (uint32_t)r) : 32 + word_select(hi, (uint32_t)(r - plo));
-        }
-        const int got = __shfl((int)k, src, 64);
-        if (r >= 0 && r < pc && lane < GW_BS_LIST) my_pos = got;
-      }
-      if (ndir && (base % kDirBits) == 0 && lane == 0) dir[base / kDirBits] = c;
-      if (lane == 0) {
-        bits[base / 32] = (uint32_t)m;
-        if (base + 32 < d) bits[base / 32 + 1] = (uint32_t)(m >> 32);
-      }
-      c += (uint32_t)__popcll(m);
-    }
-    // kp: the lane that saw u
-    const unsigned long long km = __ballot(kp_local >= 0);
-    int kp = -1;
-    if (km) {
-      const int src = __ffsll(km) - 1;
-      kp = __shfl(kp_local, src, 64);
-    }
-    if (gw_bs_is_list(c, (uint32_t)d)) {
-      __threadfence();  // inline bit words written above by lane 0 land first
-      if (lane < GW_BS_LIST) reinterpret_cast<uint16_t*>(bsn[e].w)[lane] = (uint16_t)my_pos;
-    } else if (gw_bs_is_ef(c, (uint32_t)d) && lane == 0) {
-      // Elias-Fano from the region bits lane 0 wrote above (same thread: visible)
-      const int l = gw_bs_ef_l(c, (uint32_t)d);
-      const uint32_t U = c + (uint32_t)((d - 1) >> l) + 1;
-      uint32_t ef[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-      uint32_t idx = 0;
-      for (int64_t w = 0; w < (d + 31) / 32; ++w)
-        for (uint32_t x = bits[w]; x; x &= x - 1) {
-          const uint32_t p = (uint32_t)(32 * w + __ffs(x) - 1);
-          const uint32_t up = (p >> l) + idx;  // high part, unary
-          ef[up >> 5] |= 1u << (up & 31);
-          for (int b = 0; b < l; ++b)
-            if ((p >> b) & 1u) ef[(U + idx * l + b) >> 5] |= 1u << ((U + idx * l + b) & 31);
-          ++idx;
-        }
-      for (int t = 0; t < 10; ++t) bsn[e].w[t] = ef[t];
-    }
-    if (lane == 0) {
-      bsn[e].c = c;
-      bsn[e].kp = (uint32_t)kp;
-    }
+    gw_bs_nbr* en = bsn + e;
+    const uint32_t c = en->c, d = en->d;
+    const BsEmit E = bs_emit(en, reg, roff, e, c, d);
+    if (E.mode == BS_LIST && lane >= (int)c && lane < 2 * 10) reinterpret_cast<uint16_t*>(en->w)[lane] = 0xFFFFu;
+    if (E.mode == BS_REGION && lane < 2) en->w[lane] = (uint32_t)(roff[e] >> (32 * lane));
+    int64_t klast;
+    common_wave(G, bs_slot(G, e), E, &klast);
+    if (E.mode == BS_REGION)
+      for (int64_t g = (klast < 0 ? -1 : klast / kDirBits) + 1 + lane; g < E.ndir; g += 64) E.dir[g] = c;
   }
 }
 
@@ -529,27 +678,52 @@ void gw_dev_bitset_release(gw_graph* g) {
   bs_free(g->d.bs_nbr);
 }
 
-// Build the per-edge regions.  Requires the membership bitmap (has_edge).
+// Build the per-edge entries and regions.  Requires the membership bitmap
+// (has_edge).  Regions are sized from the exact common-neighbour counts (pass
+// 1), so slots whose payload fits the entry take no region space.
 int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes) {
   gw_dev_graph& d = g->d;
   gw_dev_bitset_release(g);
   const int64_t nnz = g->nnz;
   if (nnz == 0) return GW_OK;
+  if (nnz * (int64_t)sizeof(gw_bs_nbr) > budget_bytes) {
+    g->err = "bitset entries need " + std::to_string(nnz * (int64_t)sizeof(gw_bs_nbr)) + " B; over the " +
+             std::to_string(budget_bytes) + " B budget: use GW_N2V_REJECTION";
+    return GW_ERR_CAPACITY;
+  }
   int rc;
   uint64_t* sz = nullptr;
   uint64_t* roff = nullptr;
-  if ((rc = bs_alloc(g, &sz, nnz + 1)) || (rc = bs_alloc(g, &roff, nnz + 1))) {
+  int64_t* big = nullptr;
+  unsigned long long* nbig = nullptr;
+  auto cleanup = [&]() {
     bs_free(sz);
+    bs_free(roff);
+    bs_free(big);
+    bs_free(nbig);
+  };
+  if ((rc = bs_alloc(g, &d.bs_nbr, nnz)) || (rc = bs_alloc(g, &big, nnz)) || (rc = bs_alloc(g, &nbig, 1)) ||
+      (rc = bs_alloc(g, &sz, nnz + 1)) || (rc = bs_alloc(g, &roff, nnz + 1))) {
+    cleanup();
+    gw_dev_bitset_release(g);
     return rc;
   }
-  k_bs_sizes<<<(unsigned)((nnz + kB - 1) / kB), kB>>>(nnz, d.nbrs, d.deg, sz);
+  const unsigned grid = (unsigned)((nnz + kB - 1) / kB);
+  GW_HIP_TRY(hipMemset(d.bs_nbr, 0, (size_t)nnz * sizeof(gw_bs_nbr)));
+  GW_HIP_TRY(hipMemset(nbig, 0, sizeof(unsigned long long)));
+  k_bs_count<<<grid, kB>>>(d, d.bs_nbr, big, nbig);
+  GW_HIP_TRY(hipGetLastError());
+  k_bs_count_wave<<<4096, kB>>>(d, d.bs_nbr, big, nbig);
+  GW_HIP_TRY(hipGetLastError());
+  k_bs_sizes<<<grid, kB>>>(d, d.bs_nbr, sz);
+  GW_HIP_TRY(hipGetLastError());
   GW_HIP_TRY(hipMemset(sz + nnz, 0, sizeof(uint64_t)));
   size_t tmpb = 0;
   GW_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmpb, sz, roff, nnz + 1));
   void* tmp = nullptr;
   if ((rc = bs_alloc(g, (char**)&tmp, (int64_t)tmpb + 1))) {
-    bs_free(sz);
-    bs_free(roff);
+    cleanup();
+    gw_dev_bitset_release(g);
     return rc;
   }
   GW_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmpb, sz, roff, nnz + 1));
@@ -559,33 +733,28 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes) {
   uint64_t words = 0;
   GW_HIP_TRY(hipMemcpy(&words, roff + nnz, sizeof(uint64_t), hipMemcpyDeviceToHost));
   const int64_t need = (int64_t)words * 4 + nnz * (int64_t)sizeof(gw_bs_nbr);
-  if (words == 0) words = 1;  // every bitset is inline: keep a valid region pointer
   if (need > budget_bytes) {
-    bs_free(roff);
-    g->err = "per-edge bitsets need " + std::to_string(need) + " B (sum(deg^2) bits); over the " +
-             std::to_string(budget_bytes) + " B budget: use GW_N2V_REJECTION";
+    cleanup();
+    gw_dev_bitset_release(g);
+    g->err = "per-edge bitsets need " + std::to_string(need) + " B; over the " + std::to_string(budget_bytes) +
+             " B budget: use GW_N2V_REJECTION";
     return GW_ERR_CAPACITY;
   }
-  int64_t* big = nullptr;
-  unsigned long long* nbig = nullptr;
-  if ((rc = bs_alloc(g, &d.bs_region, (int64_t)words)) || (rc = bs_alloc(g, &d.bs_nbr, nnz)) ||
-      (rc = bs_alloc(g, &big, nnz)) || (rc = bs_alloc(g, &nbig, 1))) {
-    bs_free(roff);
-    bs_free(big);
-    bs_free(nbig);
+  if (words == 0) words = 1;  // no region at all: keep a valid pointer
+  if ((rc = bs_alloc(g, &d.bs_region, (int64_t)words))) {
+    cleanup();
     gw_dev_bitset_release(g);
     return rc;
   }
   GW_HIP_TRY(hipMemset(d.bs_region, 0, (size_t)words * 4));
-  GW_HIP_TRY(hipMemset(nbig, 0, sizeof(unsigned long long)));
-  k_bs_fill_small<<<(unsigned)((nnz + kB - 1) / kB), kB>>>(d, roff, d.bs_region, d.bs_nbr, big, nbig);
+  k_bs_fill_small<<<grid, kB>>>(d, d.bs_nbr);
   GW_HIP_TRY(hipGetLastError());
-  k_bs_fill_wave<<<2048, kB>>>(d, roff, d.bs_region, d.bs_nbr, big, nbig);
+  k_bs_fill_thread<<<grid, kB>>>(d, roff, d.bs_region, d.bs_nbr);
+  GW_HIP_TRY(hipGetLastError());
+  k_bs_fill_wave<<<4096, kB>>>(d, roff, d.bs_region, d.bs_nbr, big, nbig);
   GW_HIP_TRY(hipGetLastError());
   GW_HIP_TRY(hipDeviceSynchronize());
-  bs_free(roff);
-  bs_free(big);
-  bs_free(nbig);
+  cleanup();
   g->bitset_words = (int64_t)words;
   return GW_OK;
 }

@@ -71,7 +71,8 @@ class GraphInfo(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int64), ("nnz", ctypes.c_int64),
                 ("max_degree", ctypes.c_int64), ("edge_alias_entries", ctypes.c_int64),
                 ("semantics", ctypes.c_int32), ("directed", ctypes.c_int32),
-                ("weighted", ctypes.c_int32), ("device", ctypes.c_int32)]
+                ("weighted", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("sampler_bytes", ctypes.c_int64)]
 
 
 P = ctypes.c_void_p

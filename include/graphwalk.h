@@ -88,6 +88,8 @@ typedef struct gw_graph_info_t {
   int32_t directed;
   int32_t weighted;
   int32_t device;     /* -1 when not resident                               */
+  int64_t sampler_bytes; /* HBM held by the prepared n2v sampler's per-slot tables
+                            (bitset entries + regions, or rejection slot entries) */
 } gw_graph_info_t;
 
 typedef struct gw_topsim_stats_t {
