@@ -590,9 +590,12 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
     }
   }
   if (mode == GW_N2V_BITSET && !(p == 1.0 && q == 1.0)) {
+    // budget: half of the free HBM (GW_BITSET_BUDGET_GB lowers it)
     size_t fr = 0, tot = 0;
     int64_t budget = (int64_t)64 << 30;
-    if (hipMemGetInfo(&fr, &tot) == hipSuccess) budget = std::min<int64_t>(budget, (int64_t)(fr / 2));
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) budget = (int64_t)(fr / 2);
+    if (const char* bb = getenv("GW_BITSET_BUDGET_GB"))
+      budget = std::min<int64_t>(budget, (int64_t)(atof(bb) * (double)(1 << 30)));
     if ((rc = gw_dev_bitset_build(g, budget))) return rc;
   }
   g->p = p;

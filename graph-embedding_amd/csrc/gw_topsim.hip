@@ -40,11 +40,13 @@ namespace {
 constexpr int TS_BLOCK = 512;
 constexpr int TS_WAVES = TS_BLOCK / 64;
 constexpr int TOPK_MAX = 256;
+constexpr int TS_CO_LDS = 1792;  // child / spawner offsets kept in LDS up to this many entries
 constexpr int64_t LDS_ROW_MAX_BYTES = 96 * 1024;
 
 struct TsArgs {
   gw_dev_graph G;
   int variant;
+  int diag;  // GW_DIAG_TS (timing experiments only, wrong results): 1 = walkers skip computePathSim, 2 = cheap RNG
   int sample;
   double sampled;
   double cache[16];
@@ -168,23 +170,45 @@ __device__ __forceinline__ unsigned long long dkey(double v) {
   return (unsigned long long)__double_as_longlong(v);  // v >= 0: bit order == value order
 }
 
-// MODE 0: dense LDS row; 1: LDS hash of 8192 slots (96 KB)
+// MODE 0: dense LDS row; 1: LDS hash of 8192 slots (96 KB, one workgroup per
+// CU); 2: LDS hash of 6144 slots (72 KB, two workgroups per CU)
+template <int MODE>
+struct TsHash {
+  static constexpr int SLOTS = MODE == 2 ? 6144 : 8192;
+  static constexpr int LIMIT = SLOTS * 3 / 4;  // load limit before overflowing to HBM
+  __device__ static __forceinline__ uint32_t slot(int32_t key) {
+    return (uint32_t)(((uint64_t)((uint32_t)key * 0x9E3779B1u) * (uint64_t)SLOTS) >> 32);
+  }
+  __device__ static __forceinline__ uint32_t next(uint32_t h) { return h + 1 == (uint32_t)SLOTS ? 0u : h + 1; }
+};
+
 template <int STEP, int MODE>
-__global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
+__device__ __forceinline__ void topsim_body(const TsArgs& A) {
   constexpr bool LDS_ROW = MODE == 0;
-  constexpr int HASH_BITS = 13;
-  constexpr int HASH_SLOTS = 1 << HASH_BITS;
-  constexpr int HASH_LIMIT = HASH_SLOTS * 3 / 4;  // load limit before overflowing to HBM
+  using H = TsHash<MODE>;
+  constexpr int HASH_SLOTS = H::SLOTS;
+  constexpr int HASH_LIMIT = H::LIMIT;
   constexpr int L = 2 * STEP;
   extern __shared__ double s_row[];  // LDS row (LDS_ROW) or hash values+keys
   __shared__ int s_wave[TS_WAVES + 1];
   __shared__ long long s_red[TS_WAVES];
   __shared__ int s_size[L + 2];
   __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount, s_bin, s_cum, s_exact;
-  __shared__ unsigned s_hist[256];
   __shared__ unsigned long long s_prefix, s_mask;
-  __shared__ int32_t s_sel_id[TOPK_MAX];
-  __shared__ double s_sel_val[TOPK_MAX];
+  // the output phase's selection arrays share LDS with the levels' child
+  // offsets / the walkers' spawner offsets (binary-searched per child / walker)
+  __shared__ union {
+    struct {
+      double sel_val[TOPK_MAX];
+      int32_t sel_id[TOPK_MAX];
+      unsigned hist[256];
+    } out;
+    int32_t co[TS_CO_LDS];
+  } s_u;
+  int32_t* const s_sel_id = s_u.out.sel_id;
+  double* const s_sel_val = s_u.out.sel_val;
+  unsigned* const s_hist = s_u.out.hist;
+  int32_t* const s_co = s_u.co;
 
   const int tid = threadIdx.x;
   const int64_t blk = blockIdx.x;
@@ -254,7 +278,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
       atomicAdd(&s_row[target], val);
       return;
     }
-    uint32_t h = ((uint32_t)target * 0x9E3779B1u) >> (32 - HASH_BITS);
+    uint32_t h = H::slot(target);
     for (int probe = 0; probe < HASH_SLOTS; ++probe) {
       const int32_t k = s_hkey[h];
       if (k == target) {
@@ -270,7 +294,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
           return;
         }
       }
-      h = (h + 1) & (HASH_SLOTS - 1);
+      h = H::next(h);
     }
     ov_add(target, val);
   };
@@ -294,12 +318,14 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
     ++my_upd;
   };
 
-  unsigned long long ph_t = 0, ph[5] = {0, 0, 0, 0, 0};
-  auto mark = [&](int k) {  // diagnostics only
+  __shared__ unsigned long long s_ph[11];  // diagnostics only: [10] = last timestamp
+  if (tid == 0)
+    for (int k = 0; k < 11; ++k) s_ph[k] = 0;
+  auto mark = [&](int k) {
     if (A.phase && tid == 0) {
       const unsigned long long now = __builtin_readcyclecounter();
-      if (k >= 0) ph[k] += now - ph_t;
-      ph_t = now;
+      if (k >= 0) s_ph[k] += now - s_ph[10];
+      s_ph[10] = now;
     }
   };
   for (;;) {
@@ -322,8 +348,8 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
           SL[0] = 0;
           SN[0] = 0;
           SM[0] = 1.0;
-          SF[0] = 0;
-          SF[1] = A.sample;
+          s_co[0] = 0;
+          s_co[1] = A.sample;
           s_nspawn = 1;
           s_nwalk = A.sample;
         }
@@ -367,6 +393,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
         }
         if (l == L) break;
         // expansion: child counts (enumerated) and spawners (random branch)
+        int32_t* const COx = sz + 1 <= TS_CO_LDS ? s_co : CO;
         int total_children = 0;
         int spawn_base = s_nspawn;
         for (int base = 0; base < sz; base += TS_BLOCK) {
@@ -385,7 +412,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
           int tot_c, tot_s;
           const int ex_c = block_excl_scan(cnt, s_wave, &tot_c);
           const int ex_s = block_excl_scan(sp, s_wave, &tot_s);
-          if (j < sz) CO[j] = total_children + ex_c;
+          if (j < sz) COx[j] = total_children + ex_c;
           if (sp) {
             const int k = spawn_base + ex_s;
             if (k < A.spawn_cap) {
@@ -405,7 +432,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
           if ((int64_t)total_children > cap) total_children = (int)cap + 1;  // saturate
         }
         if (tid == 0) {
-          CO[sz] = total_children;
+          COx[sz] = total_children;
           s_nspawn = spawn_base;
           if ((int64_t)total_children > cap) {
             atomicOr(A.error_flag, 1);
@@ -422,9 +449,9 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
         int64_t* On = O + (int64_t)(l + 1) * cap;
         const int64_t* Ol = O + (int64_t)l * cap;
         for (int c = tid; c < total_children; c += TS_BLOCK) {
-          const int j = upper_bound_i32(CO, sz + 1, c) - 1;
-          const int k = c - CO[j];
-          const int d = CO[j + 1] - CO[j];
+          const int j = upper_bound_i32(COx, sz + 1, c) - 1;
+          const int k = c - COx[j];
+          const int d = COx[j + 1] - COx[j];
           const gw_ts_ent e = A.ent[Ol[j] + k];  // edges.get(j), insertion order (:103-110)
           Vn[c] = e.x;
           Dn[c] = e.d;
@@ -441,17 +468,18 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
       mark(0);
       // walker index prefix over spawners (queue order)
       const int ns = s_abort ? 0 : s_nspawn;
+      int32_t* const SFx = ns + 1 <= TS_CO_LDS ? s_co : SF;
       int run = 0;
       for (int base = 0; base < ns; base += TS_BLOCK) {
         const int k = base + tid;
         const int c = (k < ns) ? SF[k] : 0;
         int tot;
         const int ex = block_excl_scan(c, s_wave, &tot);
-        if (k < ns) SF[k] = run + ex;
+        if (k < ns) SFx[k] = run + ex;
         run += tot;
       }
       if (tid == 0) {
-        SF[ns] = run;
+        SFx[ns] = run;
         s_nspawn = ns;
         s_nwalk = run;
       }
@@ -464,7 +492,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
       const int W = s_nwalk;
       const int ns = s_nspawn;
       for (int g = tid; g < W; g += TS_BLOCK) {
-        const int sp = upper_bound_i32(SF, ns + 1, g) - 1;
+        const int sp = upper_bound_i32(ns + 1 <= TS_CO_LDS ? s_co : SF, ns + 1, g) - 1;
         const int l0 = SL[sp];
         const double mw = SM[sp];
         int32_t path[L + 1], dpath[L + 1];
@@ -491,14 +519,21 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
             if (dcur == 0) {
               alive = false;
             } else {
-              gw_u4 u = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)t, 0u, A.k0, A.k1);
-              const gw_ts_ent e = A.ent[ocur + gw_bounded(u.x, (uint32_t)dcur)];  // randNeighbor
+              uint32_t ux;
+              if (A.diag & 2) {
+                ux = ((uint32_t)s * 0x9E3779B1u) ^ ((uint32_t)g * 0x85EBCA6Bu) ^ ((uint32_t)t * 0xC2B2AE35u);
+                ux ^= ux >> 15;
+                ux *= 0x2C1B3C6Du;
+              } else {
+                ux = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)t, 0u, A.k0, A.k1).x;
+              }
+              const gw_ts_ent e = A.ent[ocur + gw_bounded(ux, (uint32_t)dcur)];  // randNeighbor
               path[t] = e.x;
               dpath[t] = e.d;
               dcur = e.d;
               ocur = e.off;
               ++my_ext;
-              if ((t & 1) == 0) contrib(path, dpath, t / 2, s, mw);
+              if ((t & 1) == 0 && !(A.diag & 1)) contrib(path, dpath, t / 2, s, mw);
             }
           }
         }
@@ -516,7 +551,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
       for (int k = tid; k < nov; k += TS_BLOCK) {
         const int32_t slot = touched[k];
         const int32_t key = __hip_atomic_load(&ov_key[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t h = ((uint32_t)key * 0x9E3779B1u) >> (32 - HASH_BITS);
+        uint32_t h = H::slot(key);
         for (int probe = 0; probe < HASH_SLOTS; ++probe) {
           const int32_t kk = s_hkey[h];
           if (kk == -1) break;
@@ -526,7 +561,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
             __hip_atomic_store(&ov_val[slot], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
           }
-          h = (h + 1) & (HASH_SLOTS - 1);
+          h = H::next(h);
         }
       }
       __syncthreads();
@@ -569,6 +604,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
         if (cand(idx, &id, &v)) ++c_local;
       }
       const int C = (int)block_sum<long long>(c_local, s_red);
+      mark(5);
       unsigned long long T = 0;  // threshold key (K-th largest)
       int32_t idT = 0x7fffffff;  // largest id taken at key == T
       bool take_all = (C <= K);
@@ -611,6 +647,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
         Tmask = s_mask;
         T = s_prefix;
       }
+      mark(6);
       if (!take_all && !bin_exact) {
         // ties at the threshold: smallest ids first
         long long eq_local = 0;
@@ -650,6 +687,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
           idT = (int32_t)s_prefix;
         }
       }
+      mark(7);
       if (tid == 0) s_cnt = 0;
       __syncthreads();
       for (int idx = tid; idx < NC; idx += TS_BLOCK) {
@@ -667,6 +705,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
       }
       __syncthreads();
       const int cnt = min(s_cnt, TOPK_MAX);
+      mark(8);
       // order by (value desc, id asc): every selected entry counts the entries
       // that precede it (<= 256 entries, one pass, broadcast LDS reads)
       int32_t* oid = A.out_ids + r * (int64_t)K;
@@ -698,7 +737,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
       }
     }
     __syncthreads();
-    mark(3);
+    mark(9);
     // re-zero the accumulator for the next source
     if (LDS_ROW) {
       for (int t = tid; t < n; t += TS_BLOCK) s_row[t] = 0.0;
@@ -723,7 +762,7 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
   }
 
   if (A.phase && tid == 0)
-    for (int k = 0; k < 5; ++k) atomicAdd(&A.phase[k], ph[k]);
+    for (int k = 0; k < 10; ++k) atomicAdd(&A.phase[k], s_ph[k]);
   // statistics
   long long e = block_sum<long long>(my_ext, s_red);
   long long u = block_sum<long long>(my_upd, s_red);
@@ -734,6 +773,16 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
     atomicMax(&A.stats[2], my_maxf);
     atomicAdd((unsigned long long*)&A.stats[3], (unsigned long long)w);
   }
+}
+
+template <int STEP, int MODE>
+__global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
+  topsim_body<STEP, MODE>(A);
+}
+// two workgroups per CU (<= 72 KB dynamic LDS, <= 128 VGPRs): small dense rows and the 6144-slot hash
+template <int STEP, int MODE>
+__global__ void __launch_bounds__(TS_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) k_topsim_2wg(TsArgs A) {
+  topsim_body<STEP, MODE>(A);
 }
 
 template <typename T>
@@ -766,28 +815,37 @@ void ws_free(T*& p) {
   p = nullptr;
 }
 
-template <int STEP, int LDS>
+constexpr size_t TS_2WG_LDS = 72 * 1024;  // dynamic LDS that still lets two workgroups share a CU
+
+template <int STEP, int MODE, bool TWO>
 hipError_t launch_step(const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
-  {
-    hipError_t e = hipFuncSetAttribute((const void*)k_topsim<STEP, LDS>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
-  k_topsim<STEP, LDS><<<blocks, TS_BLOCK, lds, s>>>(A);
+  const void* fn = TWO ? (const void*)k_topsim_2wg<STEP, MODE> : (const void*)k_topsim<STEP, MODE>;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  if (TWO)
+    k_topsim_2wg<STEP, MODE><<<blocks, TS_BLOCK, lds, s>>>(A);
+  else
+    k_topsim<STEP, MODE><<<blocks, TS_BLOCK, lds, s>>>(A);
   return hipGetLastError();
 }
 
-template <int LDS>
-hipError_t launch(int step, const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
+template <int STEP>
+hipError_t launch_mode(int mode, const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
+  if (mode == 2) return launch_step<STEP, 2, true>(A, blocks, lds, s);
+  if (mode == 1) return launch_step<STEP, 1, false>(A, blocks, lds, s);
+  return lds <= TS_2WG_LDS ? launch_step<STEP, 0, true>(A, blocks, lds, s) : launch_step<STEP, 0, false>(A, blocks, lds, s);
+}
+
+hipError_t launch(int step, int mode, const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
   switch (step) {
-    case 1: return launch_step<1, LDS>(A, blocks, lds, s);
-    case 2: return launch_step<2, LDS>(A, blocks, lds, s);
-    case 3: return launch_step<3, LDS>(A, blocks, lds, s);
-    case 4: return launch_step<4, LDS>(A, blocks, lds, s);
-    case 5: return launch_step<5, LDS>(A, blocks, lds, s);
-    case 6: return launch_step<6, LDS>(A, blocks, lds, s);
-    case 7: return launch_step<7, LDS>(A, blocks, lds, s);
-    case 8: return launch_step<8, LDS>(A, blocks, lds, s);
+    case 1: return launch_mode<1>(mode, A, blocks, lds, s);
+    case 2: return launch_mode<2>(mode, A, blocks, lds, s);
+    case 3: return launch_mode<3>(mode, A, blocks, lds, s);
+    case 4: return launch_mode<4>(mode, A, blocks, lds, s);
+    case 5: return launch_mode<5>(mode, A, blocks, lds, s);
+    case 6: return launch_mode<6>(mode, A, blocks, lds, s);
+    case 7: return launch_mode<7>(mode, A, blocks, lds, s);
+    case 8: return launch_mode<8>(mode, A, blocks, lds, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -844,8 +902,14 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
     g->err = "unknown TopSim variant";
     return GW_ERR_INVALID;
   }
-  const bool lds_row = n * 8 <= LDS_ROW_MAX_BYTES;
-  const int mode = lds_row ? 0 : 1;
+  bool lds_row = n * 8 <= LDS_ROW_MAX_BYTES;
+  int mode = lds_row ? 0 : 2;
+  if (const char* hm = std::getenv("GW_DIAG_TS_HASH")) {  // A/B knob: force the 8192- (1) or 6144-slot (2) hash
+    if (hm[0] == '1' || hm[0] == '2') {
+      mode = hm[0] - '0';
+      lds_row = false;
+    }
+  }
   // hash mode: HBM overflow table per workgroup (power of two) beyond the
   // 6144 keys the LDS table holds; distinct targets per source are bounded by
   // min(n, pair updates <= ~3*STEP*SAMPLE)
@@ -861,7 +925,7 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, g->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
   const int64_t budget = (int64_t)16 << 30;  // 16 GB of the 288 GB HBM
-  int64_t blocks = std::min<int64_t>(4 * dev_cus, budget / std::max<int64_t>(per_block, 1));
+  int64_t blocks = std::min<int64_t>(4 * dev_cus, budget / std::max<int64_t>(per_block, 1));  // persistent
   if (variant == GW_TOPSIM_ENUMERATE) blocks = std::min<int64_t>(blocks, dev_cus);
   if (blocks < 1) {
     g->err = "TopSim workspace exceeds the 16 GB budget";
@@ -901,7 +965,7 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   t.spawn_cap = spawn_cap;
   t.touch_cap = touch_cap;
   t.lds_row = mode;
-  t.lds_bytes = lds_row ? (size_t)n * 8 : (size_t)8192 * 12;
+  t.lds_bytes = lds_row ? (size_t)n * 8 : (size_t)(mode == 2 ? TsHash<2>::SLOTS : TsHash<1>::SLOTS) * 12;
   GW_HIP_TRY(hipDeviceSynchronize());
   return GW_OK;
 }
@@ -921,6 +985,10 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   TsArgs A;
   A.G = g->d;
   A.variant = variant;
+  {
+    const char* dg = std::getenv("GW_DIAG_TS");
+    A.diag = dg ? std::atoi(dg) : 0;
+  }
   A.sample = sample;
   A.sampled = (double)sample;
   for (int i = 0; i < 16; ++i) A.cache[i] = 0.0;
@@ -960,11 +1028,10 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   const char* dph = std::getenv("GW_DIAG_TS_PHASES");
   A.phase = nullptr;
   if (dph && dph[0] == '1') {
-    GW_HIP_TRY(hipMalloc((void**)&A.phase, 5 * sizeof(unsigned long long)));
-    GW_HIP_TRY(hipMemsetAsync(A.phase, 0, 5 * sizeof(unsigned long long), s));
+    GW_HIP_TRY(hipMalloc((void**)&A.phase, 10 * sizeof(unsigned long long)));
+    GW_HIP_TRY(hipMemsetAsync(A.phase, 0, 10 * sizeof(unsigned long long), s));
   }
-  hipError_t e = t.lds_row == 0 ? launch<0>(step, A, blocks, t.lds_bytes, s)
-                                 : launch<1>(step, A, blocks, t.lds_bytes, s);
+  hipError_t e = launch(step, t.lds_row, A, blocks, t.lds_bytes, s);
   if (e != hipSuccess) {
     g->err = std::string("k_topsim launch: ") + hipGetErrorString(e);
     return GW_ERR_DEVICE;
@@ -973,11 +1040,13 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   GW_HIP_TRY(hipMemcpyAsync(&flag, t.error_flag, sizeof(int), hipMemcpyDeviceToHost, s));
   GW_HIP_TRY(hipStreamSynchronize(s));
   if (A.phase) {
-    unsigned long long ph[5];
+    unsigned long long ph[10];
     GW_HIP_TRY(hipMemcpy(ph, A.phase, sizeof ph, hipMemcpyDeviceToHost));
     (void)hipFree(A.phase);
     std::fprintf(stderr, "[k_topsim phases, cycles summed over %d blocks] levels %llu walkers %llu output %llu "
-                 "clear %llu (spawn-prefix %llu)\n", blocks, ph[0] + 0ull, ph[2], ph[3], ph[4], ph[1]);
+                 "(count %llu radix %llu ties %llu collect %llu order %llu) clear %llu (spawn-prefix %llu)\n",
+                 blocks, ph[0] + 0ull, ph[2], ph[3] + ph[5] + ph[6] + ph[7] + ph[8] + ph[9], ph[5], ph[6], ph[7],
+                 ph[8], ph[9], ph[4], ph[1]);
   }
   if (flag) {
     g->err = "TopSim frontier exceeded the workspace (level/spawn/touch capacity)";
