@@ -257,3 +257,55 @@ def test_bitset_refused_for_weighted_or_directed(gw):
     G = gw.GWGraph.from_edgelist(os.path.join(DATA, "weighted_quirks.edgelist"), " ", "nx", False, True).to_device(0)
     with pytest.raises(C.UnsupportedError):
         C.check(C.lib().gw_n2v_prepare(G.handle, 0.5, 2.0, C.N2V_BITSET), G.handle)
+
+
+def _mixed_mode_edgelist(path):
+    """Unweighted graph whose slots exercise every bitset payload and build
+    path: superhubs (deg ~2000) and a dense core (deg ~300-400) give region
+    payloads built by the wave kernel from either row; periphery vertices
+    (deg 25-60) give list / Elias-Fano / region payloads built by one thread
+    from the shorter row; self-loops on hubs, core and periphery."""
+    rng = np.random.default_rng(2024)
+    n, hubs, core = 2600, 10, 600
+    E = set()
+    for h in range(hubs):
+        for v in np.nonzero(rng.random(n) < 0.8)[0]:
+            if v != h:
+                E.add((min(h, v), max(h, v)))
+    for i in range(hubs, core):
+        for j in np.nonzero(rng.random(core - i - 1) < 0.5)[0] + i + 1:
+            E.add((i, int(j)))
+    for u in range(core, n):
+        for v in rng.choice(n, int(rng.integers(25, 61)), replace=False):
+            if v != u:
+                E.add((min(u, int(v)), max(u, int(v))))
+    for v in list(range(0, 5)) + list(range(10, 41)) + list(range(600, 611)):
+        E.add((v, v))
+    with open(path, "w") as f:
+        for a, b in sorted(E):
+            f.write(f"{a} {b}\n")
+
+
+@pytest.mark.parametrize("p,q", [(0.25, 4), (4, 0.25)])
+def test_bitset_mixed_payload_modes_equal_oracle(gw, oracle, tmp_path, p, q):
+    import torch
+    from gwamd import _lib as C
+    path = str(tmp_path / "mixed.edgelist")
+    _mixed_mode_edgelist(path)
+    G = gw.GWGraph.from_edgelist(path, " ", "nx").to_device(0)
+    C.check(C.lib().gw_n2v_prepare(G.handle, float(p), float(q), C.N2V_BITSET), G.handle)
+    info = G.info()
+    assert info.sampler_bytes > info.nnz * 64  # some slots hold regions
+    n, L = G.n, 30
+    begin, count = 123, 20000
+    out = torch.empty((count, L), dtype=torch.int32, device="cuda")
+    lens = torch.empty(count, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    C.check(C.lib().gw_n2v_walks(G.handle, L, 5, begin, count, 1, C.ptr(out), C.ptr(lens), C.ptr(cnt), None),
+            G.handle)
+    torch.cuda.synchronize()
+    ref, rl, rc = oracle.walks_bitset(G.export_csr(), p, q, 5, L, begin, count, nthreads=8)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    np.testing.assert_array_equal(lens.cpu().numpy(), rl)
+    assert int(cnt[0]) == int(rc[0]) and int(cnt[1]) == int(rc[1])
+    assert n == 2600
