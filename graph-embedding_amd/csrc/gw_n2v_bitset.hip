@@ -19,10 +19,15 @@
 //
 // Per edge slot s = (u -> v):
 //   bs_nbr[s] (64 B, one HBM sector): v, d = deg(v), offsets[v] (int64),
-//            kp (position of u in N(v)), c, and either the bitset itself
-//            (d <= 320, inline) or the word offset of its region
-//   region   (d > 320 only) dir[ndir]  cumulative set bits before each
-//                       512-bit block (d > 512 only), then
+//            kp (position of u in N(v)), c, and a 40 B payload: the common
+//            positions (u16 list or Elias-Fano), the bitset itself (d <= 320),
+//            or for a region: w[0] = its 64 B block index, w[1..4] = the
+//            directory (u16 counts, d <= 4096), w[5..9] = a 160-bucket filter
+//            over the draw u (bucket = u*160 >> 32; bit set iff some u in the
+//            bucket lands on a common position), so most "other"-branch
+//            membership tests never read the region
+//   region   (d > 320, payload full) dir[ndir]  cumulative set bits before
+//                       each 512-bit block (d > 4096 only), then
 //            bits[ceil(d/32)]  bit k = (N(v)[k] != u) && has_edge(N(v)[k], u)
 // The entry chosen by a step carries everything the next step needs, so a
 // step into a vertex of degree <= 320 touches ONE random sector (the entry);
@@ -43,10 +48,15 @@ constexpr int kDirBits = 512;    // bits per directory block
 constexpr int kSmallD = 32;      // thread-per-slot fill up to this degree
 constexpr int kStage = 16;
 
+constexpr int kPDir = 8;         // region entries with <= this many directory blocks keep the directory in the entry
+constexpr uint32_t kFilt = 160;  // coarse filter buckets in a region entry (w[5..9])
+
 __host__ __device__ __forceinline__ int64_t bs_ndir(int64_t d) { return d > kDirBits ? (d + kDirBits - 1) / kDirBits : 0; }
 __host__ __device__ __forceinline__ int64_t bs_round(int64_t w) { return (w + kBlk - 1) / kBlk * kBlk; }
-// word offset of the bits inside a region (the directory is padded to a block)
-__host__ __device__ __forceinline__ int64_t bs_boff(int64_t d) { return d <= GW_BS_INLINE_BITS ? 0 : bs_round(bs_ndir(d)); }
+// word offset of the bits inside a region (a directory kept in the region is padded to a block)
+__host__ __device__ __forceinline__ int64_t bs_boff(int64_t d) {
+  return (d <= GW_BS_INLINE_BITS || bs_ndir(d) <= kPDir) ? 0 : bs_round(bs_ndir(d));
+}
 __host__ __device__ __forceinline__ int64_t bs_words(int64_t d) {
   return d <= GW_BS_INLINE_BITS ? 0 : bs_boff(d) + bs_round((d + 31) / 32);
 }
@@ -202,9 +212,11 @@ __device__ uint32_t common_wave(const gw_dev_graph& G, const BsSlot& S, F&& f, i
 struct BsEmit {
   int mode;
   uint32_t* w;     // entry payload
-  uint32_t* dir;   // region directory (ndir > 0)
+  uint32_t* dir;   // region directory (ndir > kPDir)
+  uint16_t* pdir;  // directory in the entry (0 < ndir <= kPDir)
   uint32_t* bits;  // region bits
   int64_t ndir;
+  uint32_t d;
   int l;
   uint32_t U;
   __device__ void operator()(int64_t k, uint32_t idx, int64_t kprev) const {
@@ -223,8 +235,22 @@ struct BsEmit {
       }
     } else {
       atomicOr(&bits[k >> 5], bit);
-      if (ndir > 0)  // dir[g] = #positions below block g
-        for (int64_t g = (kprev < 0 ? -1 : kprev / kDirBits) + 1; g <= k / kDirBits; ++g) dir[g] = idx;
+      set_dir((kprev < 0 ? -1 : kprev / kDirBits) + 1, k / kDirBits, idx);
+      // filter: the draws u with floor(u*d / 2^32) == k span at most two buckets
+      const uint64_t ulo = (((uint64_t)k << 32) + d - 1) / d;
+      const uint64_t uhi = ((((uint64_t)k + 1) << 32) + d - 1) / d - 1;
+      const uint32_t b0 = gw_bounded((uint32_t)ulo, kFilt), b1 = gw_bounded((uint32_t)uhi, kFilt);
+      for (uint32_t b = b0; b <= b1; ++b) atomicOr(&w[5 + (b >> 5)], 1u << (b & 31));
+    }
+  }
+  // directory blocks [g0, g1] start after `count` common positions
+  __device__ void set_dir(int64_t g0, int64_t g1, uint32_t count) const {
+    if (ndir == 0) return;
+    for (int64_t g = g0; g <= g1 && g < ndir; ++g) {
+      if (pdir)
+        pdir[g] = (uint16_t)count;
+      else
+        dir[g] = count;
     }
   }
 };
@@ -236,15 +262,21 @@ __device__ __forceinline__ BsEmit bs_emit(gw_bs_nbr* en, uint32_t* reg, const ui
   E.w = en->w;
   E.ndir = 0;
   E.dir = E.bits = nullptr;
+  E.pdir = nullptr;
+  E.d = d;
   E.l = 0;
   E.U = 0;
   if (E.mode == BS_EF) {
     E.l = gw_bs_ef_l(c, d);
     E.U = c + ((d - 1) >> E.l) + 1;
   } else if (E.mode == BS_REGION) {
+    E.ndir = bs_ndir(d);
     E.dir = reg + roff[e];
     E.bits = E.dir + bs_boff(d);
-    E.ndir = bs_ndir(d);
+    if (E.ndir <= kPDir) {
+      E.pdir = reinterpret_cast<uint16_t*>(en->w + 1);
+      E.dir = nullptr;
+    }
   }
   return E;
 }
@@ -347,16 +379,14 @@ __global__ void k_bs_fill_thread(gw_dev_graph G, const uint64_t* __restrict__ ro
   if (E.mode == BS_LIST) {
     for (uint32_t t = c; t < 2 * 10; ++t) reinterpret_cast<uint16_t*>(en->w)[t] = 0xFFFFu;
   } else if (E.mode == BS_REGION) {
-    en->w[0] = (uint32_t)roff[e];
-    en->w[1] = (uint32_t)(roff[e] >> 32);
+    en->w[0] = (uint32_t)(roff[e] / kBlk);  // regions are block aligned: 32-bit block index
   }
   int64_t klast = -1;
   common_thread(G, S, [&](int64_t k, uint32_t idx, int64_t kprev) {
     E(k, idx, kprev);
     klast = k;
   });
-  if (E.mode == BS_REGION)
-    for (int64_t g = (klast < 0 ? -1 : klast / kDirBits) + 1; g < E.ndir; ++g) E.dir[g] = c;
+  if (E.mode == BS_REGION) E.set_dir((klast < 0 ? -1 : klast / kDirBits) + 1, E.ndir - 1, c);
 }
 
 // pass 2, one wave per queued slot
@@ -373,11 +403,11 @@ __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff
     const uint32_t c = en->c, d = en->d;
     const BsEmit E = bs_emit(en, reg, roff, e, c, d);
     if (E.mode == BS_LIST && lane >= (int)c && lane < 2 * 10) reinterpret_cast<uint16_t*>(en->w)[lane] = 0xFFFFu;
-    if (E.mode == BS_REGION && lane < 2) en->w[lane] = (uint32_t)(roff[e] >> (32 * lane));
+    if (E.mode == BS_REGION && lane == 0) en->w[0] = (uint32_t)(roff[e] / kBlk);
     int64_t klast;
     common_wave(G, bs_slot(G, e), E, &klast);
     if (E.mode == BS_REGION)
-      for (int64_t g = (klast < 0 ? -1 : klast / kDirBits) + 1 + lane; g < E.ndir; g += 64) E.dir[g] = c;
+      for (int64_t g = (klast < 0 ? -1 : klast / kDirBits) + 1 + lane; g < E.ndir; g += 64) E.set_dir(g, g, c);
   }
 }
 
@@ -417,27 +447,39 @@ __device__ __forceinline__ int64_t inl_select(const uint32_t* __restrict__ w, ui
 
 // j-th set bit of a region bitset (c set bits): the 512-bit block comes from
 // the directory by interpolation (set bits are spread over the row), then
-// the block is read as one 64 B sector and searched in registers
-__device__ __forceinline__ int64_t bs_select(const uint32_t* __restrict__ h, int64_t d, uint32_t c, uint32_t j) {
+// the block is read as one 64 B sector and searched in registers.  Up to
+// kPDir blocks the directory is the entry's payload (registers, no read).
+template <class Dir>
+__device__ __forceinline__ int64_t dir_block(Dir dir, int64_t ndir, uint32_t c, uint32_t* j) {
+  int64_t g = (int64_t)((uint64_t)*j * (uint64_t)ndir / c);
+  if (g >= ndir) g = ndir - 1;
+  uint32_t lo = dir(g);
+  uint32_t hi = g + 1 < ndir ? dir(g + 1) : c;
+  while (lo > *j) {
+    --g;
+    hi = lo;
+    lo = dir(g);
+  }
+  while (hi <= *j) {
+    ++g;
+    lo = hi;
+    hi = g + 1 < ndir ? dir(g + 1) : c;
+  }
+  *j -= lo;
+  return g;
+}
+
+__device__ __forceinline__ uint32_t pick10(const uint32_t (&pl)[10], uint32_t idx);
+
+__device__ __forceinline__ int64_t bs_select(const uint32_t (&pl)[10], const uint32_t* __restrict__ h, int64_t d,
+                                             uint32_t c, uint32_t j) {
   const int64_t ndir = bs_ndir(d);
   int64_t g = 0;
-  if (ndir > 0) {
-    g = (int64_t)((uint64_t)j * (uint64_t)ndir / c);
-    if (g >= ndir) g = ndir - 1;
-    uint32_t lo = h[g];
-    uint32_t hi = g + 1 < ndir ? h[g + 1] : c;
-    while (lo > j) {
-      --g;
-      hi = lo;
-      lo = h[g];
-    }
-    while (hi <= j) {
-      ++g;
-      lo = hi;
-      hi = g + 1 < ndir ? h[g + 1] : c;
-    }
-    j -= lo;
-  }
+  if (ndir > kPDir)
+    g = dir_block([&](int64_t x) { return h[x]; }, ndir, c, &j);
+  else if (ndir > 0)
+    g = dir_block([&](int64_t x) { return (pick10(pl, 1 + (uint32_t)(x >> 1)) >> (16 * (x & 1))) & 0xFFFFu; }, ndir, c,
+                  &j);
   const uint4* blk = reinterpret_cast<const uint4*>(h + bs_boff(d) + g * kBlk);
   uint32_t wd[kBlk];
 #pragma unroll
@@ -575,22 +617,24 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
               : lst        ? (int64_t)((pick10(pl, j >> 1) >> (16 * (j & 1))) & 0xFFFFu)
               : inl        ? (int64_t)regs_select<10>(pl, j)
               : efm        ? ef_select(pl, efU, efl, j)
-                           : bs_select(h, d, c, j);
+                           : bs_select(pl, h, d, c, j);
         } else {
           k = (int64_t)gw_bounded(u.y, (uint32_t)d);
+          const uint32_t fb = gw_bounded(u.y, kFilt);
           const bool common = (P.diag & 2) ? false
                               : lst ? list_has(pl, (uint32_t)k)
                               : inl ? ((pick10(pl, (uint32_t)(k >> 5)) >> (k & 31)) & 1u)
                               : efm ? ef_has(pl, c, efU, efl, (uint32_t)k)
-                                    : ((h[boff + (k >> 5)] >> (k & 31)) & 1u);
+                              : ((pick10(pl, 5 + (fb >> 5)) >> (fb & 31)) & 1u) && ((h[boff + (k >> 5)] >> (k & 31)) & 1u);
           acc = (k != (int64_t)kp) && !common;
         }
       } else {  // retry of the "other" branch
         k = (int64_t)gw_bounded(u.y, (uint32_t)d);
+        const uint32_t fb = gw_bounded(u.y, kFilt);
         const bool common = lst ? list_has(pl, (uint32_t)k)
                             : inl ? ((pick10(pl, (uint32_t)(k >> 5)) >> (k & 31)) & 1u)
                             : efm ? ef_has(pl, c, efU, efl, (uint32_t)k)
-                                  : ((h[boff + (k >> 5)] >> (k & 31)) & 1u);
+                            : ((pick10(pl, 5 + (fb >> 5)) >> (fb & 31)) & 1u) && ((h[boff + (k >> 5)] >> (k & 31)) & 1u);
         acc = ((k != (int64_t)kp) && !common) || trial >= (1u << 24);
       }
       if (acc) {
@@ -612,7 +656,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
           efl = gw_bs_ef_l(c, (uint32_t)d);
           efU = c + (uint32_t)((d - 1) >> efl) + 1;
         }
-        h = (lst || inl || efm) ? en->w : G.bs_region + ((uint64_t)e1.z | ((uint64_t)e1.w << 32));
+        h = (lst || inl || efm) ? en->w : G.bs_region + (uint64_t)e1.z * kBlk;
         boff = (uint32_t)bs_boff(d);
         pl[0] = e1.z; pl[1] = e1.w; pl[2] = e2.x; pl[3] = e2.y; pl[4] = e2.z;
         pl[5] = e2.w; pl[6] = e3.x; pl[7] = e3.y; pl[8] = e3.z; pl[9] = e3.w;
