@@ -566,16 +566,50 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       }
       __syncthreads();
     }
-    const int NC = LDS_ROW ? n : HASH_SLOTS + nov;
+    // hash mode: move the occupied LDS slots to the front once, so the
+    // selection passes below scan only them (the others are left empty)
+    int NL = 0;
+    if (!LDS_ROW) {
+      constexpr int SPT = HASH_SLOTS / TS_BLOCK;
+      static_assert(HASH_SLOTS % TS_BLOCK == 0, "hash slots per thread");
+      int32_t kk[SPT];
+      double vv[SPT];
+      int mine = 0;
+#pragma unroll
+      for (int i = 0; i < SPT; ++i) {
+        kk[i] = s_hkey[tid + i * TS_BLOCK];
+        vv[i] = s_hval[tid + i * TS_BLOCK];
+        mine += kk[i] != -1;
+      }
+      int tot;
+      int o = block_excl_scan(mine, s_wave, &tot);  // its barriers order every read before the writes
+#pragma unroll
+      for (int i = 0; i < SPT; ++i)
+        if (kk[i] != -1) {
+          s_hkey[tid + i * TS_BLOCK] = -1;
+          s_hval[tid + i * TS_BLOCK] = 0.0;
+        }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < SPT; ++i)
+        if (kk[i] != -1) {
+          s_hkey[o] = kk[i];
+          s_hval[o] = vv[i];
+          ++o;
+        }
+      __syncthreads();
+      NL = tot;
+    }
+    const int NC = LDS_ROW ? n : NL + nov;
     auto cand = [&](int idx, int32_t* id, double* val) -> bool {
       if (LDS_ROW) {
         *id = idx;
         *val = s_row[idx];
-      } else if (idx < HASH_SLOTS) {
+      } else if (idx < NL) {
         *id = s_hkey[idx];
         *val = s_hval[idx];
       } else {
-        const int32_t slot = touched[idx - HASH_SLOTS];
+        const int32_t slot = touched[idx - NL];
         *id = __hip_atomic_load(&ov_key[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *val = __hip_atomic_load(&ov_val[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -720,6 +754,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         if (i < cnt) {
           vi = s_sel_val[i];
           ii = s_sel_id[i];
+#pragma unroll 4
           for (int j = sub; j < cnt; j += G) {
             const double vj = s_sel_val[j];
             rank += (vj > vi) || (vj == vi && s_sel_id[j] < ii);
@@ -742,7 +777,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     if (LDS_ROW) {
       for (int t = tid; t < n; t += TS_BLOCK) s_row[t] = 0.0;
     } else {
-      for (int j = tid; j < HASH_SLOTS; j += TS_BLOCK) {
+      for (int j = tid; j < NL; j += TS_BLOCK) {  // occupied slots were compacted to [0, NL)
         s_hval[j] = 0.0;
         s_hkey[j] = -1;
       }
