@@ -22,12 +22,14 @@ Also reported (same JSON line):
                 the committed rocprofv3 PMC pass (profiles/), or null.
   cpu_baseline  the oracle's C restatement of the same sampling (OpenMP),
                 timed on a bounded sample of the same workload (rank 0, N=1).
-  secondary     TopSim_singleSample on lshrank blog (STEP=5, SAMPLE=10000,
-                C=0.6, top-20, all 10,313 sources): pair-updates/s; and
-                secondary.simrank_naive: SimRank.java (STEP=3, C=0.6) on blog,
-                dense 10,313^2 fp64 result: rounds/s, LDS-gather roofline;
-                secondary.walk_10m: the north_star's 10M-node/100M-edge graph
-                (R-MAT scale 24, ef 6), 1 walk per node, with its CPU sample.
+  secondary     .topsim: TopSim_singleSample on lshrank blog (STEP=5,
+                SAMPLE=10000, C=0.6, top-20, all 10,313 sources): pair-updates/s
+                (--topsim-graphs adds arxiv / moreno / p10m under .topsim.more);
+                .walk_10m / .walk_10m_p1q1: the north_star's 10M-node/100M-edge
+                graph (R-MAT scale 24, ef 6), 1 walk per node, at the bench's
+                p/q and at p=q=1, each with its CPU sample;
+                .simrank_naive: SimRank.java (STEP=3, C=0.6) on blog, dense
+                10,313^2 fp64 result: rounds/s, LDS-gather roofline.
 """
 import argparse
 import json
@@ -362,13 +364,13 @@ def main():
                          "kernel": f"k_topsim<{step},*>", "kernel_ms": kt * 1e3},
         }
 
-    secondary = None
+    secondary = {}
     if not args.no_topsim:
         names = args.topsim_graphs.split(",")
         res = [run_topsim(nm) for nm in names]
-        secondary = res[0]
+        secondary["topsim"] = res[0]
         if len(res) > 1:
-            secondary["more"] = res[1:]
+            secondary["topsim"]["more"] = res[1:]
 
     # ---- naive SimRank (SimRank.java) on the GPU: the TopSim ground truth ----
     def run_simrank(name):
@@ -508,8 +510,6 @@ def main():
         BG = gwamd.GWGraph.rmat(args.walk10m_scale, args.walk10m_edge_factor, 0.57, 0.19, 0.19, args.seed + 1)
         build_s = time.perf_counter() - t0
         BG.to_device(dev.index)
-        if secondary is None:
-            secondary = {}
         # the bench's p/q, then p=q=1 (the north_star graph walked first-order)
         secondary["walk_10m"] = run_walk10m(BG, build_s, args.p, args.q)
         secondary["walk_10m_p1q1"] = run_walk10m(BG, build_s, 1.0, 1.0)
@@ -517,10 +517,7 @@ def main():
 
     if not args.no_simrank:
         sr = run_simrank(args.simrank_graph)
-        if secondary is None:
-            secondary = {"simrank_naive": sr}
-        else:
-            secondary["simrank_naive"] = sr
+        secondary["simrank_naive"] = sr
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -556,7 +553,7 @@ def main():
                          "bytes_per_unit": BYTES_PER_STEP, "units_per_launch": launch_steps,
                          "lib_sha256": lib_digest(), "random_line_roofline": line_rate},
             "cpu_baseline": cpu,
-            "secondary": secondary,
+            "secondary": secondary or None,
         }
         print(json.dumps(res), flush=True)
     if world > 1:

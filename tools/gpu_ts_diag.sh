@@ -8,6 +8,6 @@ for dg in ${DIAGS:-0 1 2 3}; do
   GW_DIAG_TS=$dg GW_DIAG_TS_PHASES=1 timeout -k 10 600 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-simrank --no-walk10m --topsim-graphs $GRAPHS > gpurun_out/tsd_$dg.json 2> gpurun_out/tsd_$dg.err || { echo FAIL $dg; tail -5 gpurun_out/tsd_$dg.err; exit 1; }
   echo "diag $dg: $(grep phases gpurun_out/tsd_$dg.err | tail -1)"
   python -c "
-import json; d=json.load(open('gpurun_out/tsd_$dg.json'))['secondary']
+import json; d=json.load(open('gpurun_out/tsd_$dg.json'))['secondary']['topsim']
 for r in [d]+d.get('more',[]): print('   ', r['config']['workload'][:30], round(r['roofline']['kernel_ms'],2), 'ms')"
 done
