@@ -563,50 +563,81 @@ struct BsParams {
   uint32_t diag;  // timing experiments only (GW_DIAG_BS): 1 = no select, 2 = no membership test
 };
 
+// round j of a cooperative entry load: lane l fetches 16 B piece (l & 3) of
+// the entry of the walker in lane 16 j + (l >> 2) (none if that walker
+// fetches nothing)
+__device__ __forceinline__ uint4 coop_piece(const uint4* __restrict__ ents, uint32_t slot, int lane, int j) {
+  const uint32_t sj = (uint32_t)__shfl((int)slot, 16 * j + (lane >> 2), 64);
+  uint4 r = make_uint4(0u, 0u, 0u, 0u);
+  if (sj != 0xFFFFFFFFu) r = ents[(uint64_t)sj * 4u + (uint32_t)(lane & 3)];
+  return r;
+}
+
+// Entry reads are cooperative: a lane's 64 B entry read as four per-lane
+// dwordx4 loads touches 64 random pages per instruction, which past ~3 GB of
+// tables runs at 2e10 sectors/s (address translation bound, measured with
+// tools/calib/calib_sweep.hip) against 4.9e10 when each instruction covers
+// 16 sectors x 64 B.  So in round j lanes 4m..4m+3 load the four 16 B pieces
+// of walker 16j+m's entry, and the pieces reach their walker through a 1 KB
+// per-wave LDS exchange.  The walk loop is therefore wave-uniform (lanes
+// whose walk is done idle in it until every lane of the wave is done).
 __global__ void __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(8, 8)))
 k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t walk_count, int shuffle,
               int32_t* __restrict__ out, int32_t* __restrict__ lens, unsigned long long* __restrict__ counters) {
   __shared__ int32_t s_stage[kB / 64][kStage][64];
+  __shared__ uint4 s_ex[kB / 64][64];
   const int lane = threadIdx.x & 63;
-  int32_t* stage = &s_stage[threadIdx.x >> 6][0][lane];
+  const int wv = threadIdx.x >> 6;
+  int32_t* stage = &s_stage[wv][0][lane];
+  uint4* ex = s_ex[wv];
+  const uint4* __restrict__ ents = reinterpret_cast<const uint4*>(G.bs_nbr);
 
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long my_steps = 0, my_trials = 0;
-  if (i < walk_count) {
-    const int64_t w = walk_begin + i;
+  const bool valid = i < walk_count;
+  unsigned long long my_steps = 0;
+  uint32_t my_trials = 0;
+  const int64_t w = walk_begin + (valid ? i : 0);
+  int32_t cur = -1;
+  int len = L;  // lanes past walk_count take no step
+  if (valid) {
     const uint64_t it = (uint64_t)w / (uint64_t)G.n;
     const uint64_t pos = (uint64_t)w % (uint64_t)G.n;
     const uint64_t sp = shuffle ? gw_feistel_perm(pos, (uint64_t)G.n, P.pk0, P.pk1, (uint32_t)it) : pos;
-    int32_t cur = G.order[sp];
-    int32_t prev = -1;
-    int32_t* row = out + i * (int64_t)L;
-    const bool vec_ok = (L & 3) == 0;
-    const uint32_t c0 = (uint32_t)w, c1 = (uint32_t)((uint64_t)w >> 32);
-    stage[0] = cur;
-    int len = 1;
-    uint32_t trial = 0;
-    // bitset of edge (prev -> cur): inside its entry (deg(cur) <= 320: the
-    // entry's sector is already in L2, so reading a word is an L2 hit) or in
-    // the region store
-    const uint32_t* h = nullptr;
-    int64_t b = G.offsets[cur], d = G.offsets[cur + 1] - b;  // row of cur
-    uint32_t c = 0, kp = 0, boff = 0;
-    bool inl = true, lst = false, efm = false;
-    uint32_t efU = 0;
-    int efl = 0;
-    uint32_t pl[10];  // entry payload: the common-neighbour list in list mode
+    cur = G.order[sp];
+    len = 1;
+  }
+  const bool vec_ok = (L & 3) == 0;
+  const uint32_t c0 = (uint32_t)w, c1 = (uint32_t)((uint64_t)w >> 32);
+  stage[0] = cur;
+  uint32_t trial = 0;
+  // bitset of edge (prev -> cur): inside its entry (deg(cur) <= 320) or in
+  // the region store at block pl[0]
+  uint32_t b = 0, d = 0;  // row of cur (slot indices < 2^32: gw_dev_bitset_build)
+  if (valid) {
+    b = (uint32_t)G.offsets[cur];
+    d = (uint32_t)(G.offsets[cur + 1] - G.offsets[cur]);
+  }
+  uint32_t c = 0, kp = 0, boff = 0;
+  bool inl = true, lst = false, efm = false;
+  uint32_t pl[10];  // entry payload
 #pragma unroll
-    for (int t = 0; t < 10; ++t) pl[t] = 0xFFFFFFFFu;
-    while (len < L) {
-      if (d == 0) break;
+  for (int t = 0; t < 10; ++t) pl[t] = 0xFFFFFFFFu;
+  for (;;) {
+    const bool active = len < L && d != 0;
+    if (__ballot(active) == 0ull) break;
+    uint32_t slot = 0xFFFFFFFFu;  // entry to fetch (accepted step)
+    if (active) {
+      const uint32_t* h = G.bs_region + (uint64_t)pl[0] * kBlk;  // region mode only
       int64_t k;
       bool acc = true;
+      const int efl = efm ? gw_bs_ef_l(c, d) : 0;  // Elias-Fano low bits and bit count
+      const uint32_t efU = efm ? c + ((d - 1) >> efl) + 1 : 0u;
       const gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
       ++trial;
       if (len == 1) {
         k = (int64_t)gw_bounded(u.x, (uint32_t)d);
       } else if (trial == 1) {
-        const double Z = (P.a_p + (double)c) + (double)(d - 1 - (int64_t)c) * P.a_q;
+        const double Z = (P.a_p + (double)c) + (double)((int64_t)d - 1 - (int64_t)c) * P.a_q;
         const double r = gw_u01(u.x) * Z;
         if (r < P.a_p) {
           k = kp;  // return to prev
@@ -617,7 +648,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
               : lst        ? (int64_t)((pick10(pl, j >> 1) >> (16 * (j & 1))) & 0xFFFFu)
               : inl        ? (int64_t)regs_select<10>(pl, j)
               : efm        ? ef_select(pl, efU, efl, j)
-                           : bs_select(pl, h, d, c, j);
+                           : bs_select(pl, h, (int64_t)d, c, j);
         } else {
           k = (int64_t)gw_bounded(u.y, (uint32_t)d);
           const uint32_t fb = gw_bounded(u.y, kFilt);
@@ -640,44 +671,53 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
       if (acc) {
         my_trials += trial;
         trial = 0;
-        const gw_bs_nbr* en = G.bs_nbr + (b + k);
-        const uint4* ep = reinterpret_cast<const uint4*>(en);
-        const uint4 e0 = ep[0], e1 = ep[1], e2 = ep[2], e3 = ep[3];  // one 64 B entry: next step's state
-        prev = cur;
-        cur = (int32_t)e0.x;
-        d = (int64_t)e0.y;
-        b = (int64_t)((uint64_t)e0.z | ((uint64_t)e0.w << 32));
-        kp = e1.x;
-        c = e1.y;
-        lst = gw_bs_is_list(c, (uint32_t)d);
-        inl = !lst && d <= GW_BS_INLINE_BITS;
-        efm = gw_bs_is_ef(c, (uint32_t)d);
-        if (efm) {
-          efl = gw_bs_ef_l(c, (uint32_t)d);
-          efU = c + (uint32_t)((d - 1) >> efl) + 1;
-        }
-        h = (lst || inl || efm) ? en->w : G.bs_region + (uint64_t)e1.z * kBlk;
-        boff = (uint32_t)bs_boff(d);
-        pl[0] = e1.z; pl[1] = e1.w; pl[2] = e2.x; pl[3] = e2.y; pl[4] = e2.z;
-        pl[5] = e2.w; pl[6] = e3.x; pl[7] = e3.y; pl[8] = e3.z; pl[9] = e3.w;
-
-        stage[64 * (len & (kStage - 1))] = cur;
-        if ((len & (kStage - 1)) == kStage - 1) {
-          int32_t* dst = row + (len - (kStage - 1));
-          if (vec_ok) {
-#pragma unroll
-            for (int j = 0; j < kStage; j += 4)
-              *reinterpret_cast<int4*>(dst + j) =
-                  make_int4(stage[64 * j], stage[64 * (j + 1)], stage[64 * (j + 2)], stage[64 * (j + 3)]);
-          } else {
-#pragma unroll
-            for (int j = 0; j < kStage; ++j) dst[j] = stage[64 * j];
-          }
-        }
-        ++len;
+        slot = b + (uint32_t)k;
       }
     }
-    (void)prev;
+    // cooperative entry load: all four rounds in flight, then the exchange
+    const uint4 r0 = coop_piece(ents, slot, lane, 0), r1 = coop_piece(ents, slot, lane, 1);
+    const uint4 r2 = coop_piece(ents, slot, lane, 2), r3 = coop_piece(ents, slot, lane, 3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ex[lane] = j == 0 ? r0 : j == 1 ? r1 : j == 2 ? r2 : r3;
+      __builtin_amdgcn_wave_barrier();
+      if ((lane >> 4) == j && slot != 0xFFFFFFFFu) {
+        const uint4* q = ex + 4 * (lane & 15);
+        const uint4 e0 = q[0], e1 = q[1], e2 = q[2], e3 = q[3];
+        cur = (int32_t)e0.x;
+        d = e0.y;
+        b = e0.z;
+        kp = e1.x;
+        c = e1.y;
+        pl[0] = e1.z; pl[1] = e1.w; pl[2] = e2.x; pl[3] = e2.y; pl[4] = e2.z;
+        pl[5] = e2.w; pl[6] = e3.x; pl[7] = e3.y; pl[8] = e3.z; pl[9] = e3.w;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (slot != 0xFFFFFFFFu) {
+      lst = gw_bs_is_list(c, (uint32_t)d);
+      inl = !lst && d <= (uint32_t)GW_BS_INLINE_BITS;
+      efm = gw_bs_is_ef(c, d);
+      boff = (uint32_t)bs_boff(d);
+
+      stage[64 * (len & (kStage - 1))] = cur;
+      if ((len & (kStage - 1)) == kStage - 1) {
+        int32_t* dst = out + i * (int64_t)L + (len - (kStage - 1));
+        if (vec_ok) {
+#pragma unroll
+          for (int j = 0; j < kStage; j += 4)
+            *reinterpret_cast<int4*>(dst + j) =
+                make_int4(stage[64 * j], stage[64 * (j + 1)], stage[64 * (j + 2)], stage[64 * (j + 3)]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < kStage; ++j) dst[j] = stage[64 * j];
+        }
+      }
+      ++len;
+    }
+  }
+  if (valid) {
+    int32_t* row = out + i * (int64_t)L;
     const int base = len & ~(kStage - 1);
     for (int t = base; t < len; ++t) row[t] = stage[64 * (t - base)];
     for (int t = len; t < L; ++t) row[t] = -1;
@@ -730,6 +770,10 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes) {
   gw_dev_bitset_release(g);
   const int64_t nnz = g->nnz;
   if (nnz == 0) return GW_OK;
+  if (nnz >= (int64_t)0xFFFFFFFF) {  // the walk kernel passes slot indices as u32
+    g->err = "bitset mode supports < 2^32 - 1 adjacency entries: use GW_N2V_REJECTION";
+    return GW_ERR_CAPACITY;
+  }
   if (nnz * (int64_t)sizeof(gw_bs_nbr) > budget_bytes) {
     g->err = "bitset entries need " + std::to_string(nnz * (int64_t)sizeof(gw_bs_nbr)) + " B; over the " +
              std::to_string(budget_bytes) + " B budget: use GW_N2V_REJECTION";
