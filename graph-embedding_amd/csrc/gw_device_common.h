@@ -67,3 +67,14 @@ __device__ __forceinline__ void gw_alias_build(double* q, JT* J, int32_t* stack,
       stack[--l_top] = large;
   }
 }
+
+// One slot entry as ONE 16 B load (a struct copy is split into a dword and a
+// dwordx3, i.e. two fabric requests for the same sector).
+__device__ __forceinline__ gw_ts_ent gw_ts_load(const gw_ts_ent* p) {
+  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  gw_ts_ent e;
+  e.x = (int32_t)v.x;
+  e.d = (int32_t)v.y;
+  e.off = (int64_t)((uint64_t)v.z | ((uint64_t)v.w << 32));
+  return e;
+}

@@ -49,7 +49,7 @@ GW_HD inline bool gw_bs_is_ef(uint32_t c, uint32_t d) {
 }
 static_assert(sizeof(gw_bs_nbr) == 64, "bitset entry must be one 64 B sector");
 
-struct gw_ts_ent {  // adjacency slot (u -> x): everything a walker's next step needs
+struct alignas(16) gw_ts_ent {  // adjacency slot (u -> x): everything a walker's next step needs
   int32_t x, d;      // neighbour, deg(x)
   int64_t off;       // offsets[x]
 };

@@ -266,7 +266,11 @@ __global__ void k_build_bitmap(int64_t n, const int64_t* __restrict__ off,
 // 4-byte store per step at a 4*L-byte lane stride.
 constexpr int kStage = 16;
 
-template <bool FIRST_ORDER, bool WEIGHTED, bool DIRECTED>
+// ENT: G.sent (16 B slot entries) exists.  A compile-time switch, not a
+// runtime test: with both paths in one body the compiler merges the two
+// neighbour-id loads into one dword load after the entry's dwordx3, which
+// serialises two dependent requests per step.
+template <bool FIRST_ORDER, bool WEIGHTED, bool DIRECTED, bool ENT>
 __global__ void __launch_bounds__(kBlock)
 k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_count,
              int shuffle, int32_t* __restrict__ out, int32_t* __restrict__ lens,
@@ -306,7 +310,14 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
         gw_u4 u = gw_philox(c0, c1, (uint32_t)len, 0u, P.k0, P.k1);
         trial = 1;
         slot = b + draw_first_order<WEIGHTED>(G, b, d, u.x, u.y);
-        next = G.nbrs[slot];
+        if (FIRST_ORDER && ENT) {  // the slot entry carries the next row
+          const gw_ts_ent en = gw_ts_load(G.sent + slot);
+          next = en.x;
+          nb = en.off;
+          nd = en.d;
+        } else {
+          next = G.nbrs[slot];
+        }
         acc = true;
       } else {
         const gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
@@ -319,8 +330,8 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
           acc = true;
         } else {
           slot = b + draw_first_order<WEIGHTED>(G, b, d, u.x, u.y);
-          if (G.sent) {  // the slot entry carries the candidate's row for the next step
-            const gw_ts_ent en = G.sent[slot];
+          if (ENT) {  // the slot entry carries the candidate's row for the next step
+            const gw_ts_ent en = gw_ts_load(G.sent + slot);
             next = en.x;
             nb = en.off;
             nd = en.d;
@@ -335,7 +346,7 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
           } else {
             bool adj;
             if (DIRECTED)
-              adj = G.sent ? gw_has_edge(G, nb, nb + nd, prev)
+              adj = ENT ? gw_has_edge(G, nb, nb + nd, prev)
                            : gw_has_edge(G, G.offsets[next], G.offsets[next + 1], prev);  // edge x -> prev
             else
               adj = gw_has_edge(G, pb, pe, next);  // x in N(prev)
@@ -378,7 +389,10 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
           }
         }
         ++len;
-        if (G.sent && !FIRST_ORDER && len > 2) {  // row of cur known: from its slot entry, or prev's row
+        if (FIRST_ORDER && ENT) {
+          b = nb;
+          e = nb + nd;
+        } else if (ENT && !FIRST_ORDER && len > 2) {  // row of cur known: from its slot entry, or prev's row
           if (slot >= 0) {
             b = nb;
             e = nb + nd;
@@ -572,13 +586,17 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
     GW_HIP_TRY(hipDeviceSynchronize());
   }
   dev_free(d.sent);
-  if (mode == GW_N2V_REJECTION && !(p == 1.0 && q == 1.0) && g->nnz) {
+  const bool fo = (p == 1.0 && q == 1.0);
+  const char* nosent = getenv("GW_DIAG_NO_SENT");  // diagnostic A/B knob only
+  if ((mode == GW_N2V_REJECTION || fo) && g->nnz && !(nosent && nosent[0] == '1')) {
     // slot entries (16 B per slot) spare the candidate's offsets[] read.  Measured: +10% at
     // R-MAT-20 (0.5 GB of entries), -6% at R-MAT-24 ef 6 (3.2 GB: 4x the footprint of nbrs[]
     // on hot hub rows, while offsets[] stays cache resident), so only up to 1 GiB.
+    // First-order walks (p = q = 1) read nothing but the slot: one random
+    // 16 B read per step instead of nbrs[] then offsets[] (any size that fits).
     size_t fr = 0, tot = 0;
     const int64_t ent_bytes = g->nnz * (int64_t)sizeof(gw_ts_ent);
-    if (ent_bytes <= ((int64_t)1 << 30) && hipMemGetInfo(&fr, &tot) == hipSuccess && (int64_t)fr / 2 > ent_bytes) {
+    if ((fo || ent_bytes <= ((int64_t)1 << 30)) && hipMemGetInfo(&fr, &tot) == hipSuccess && (int64_t)fr / 2 > ent_bytes) {
       if (dev_alloc(g, &d.sent, g->nnz) == GW_OK) {
         k_scale_ent<<<grid_for(g->nnz), kBlock>>>(d, d.sent);
         GW_HIP_TRY(hipGetLastError());
@@ -756,8 +774,15 @@ int gw_dev_n2v_walks(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int6
   hipStream_t s = (hipStream_t)stream;
   const unsigned grid = grid_for(walk_count);
   unsigned long long* C = (unsigned long long*)counters_dev;
-#define GW_LAUNCH(FO, WT, DI) \
-  k_walk_scale<FO, WT, DI><<<grid, kBlock, 0, s>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev, len_dev, C)
+#define GW_LAUNCH(FO, WT, DI)                                                                                      \
+  do {                                                                                                             \
+    if (g->d.sent)                                                                                                 \
+      k_walk_scale<FO, WT, DI, true><<<grid, kBlock, 0, s>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev, \
+                                                             len_dev, C);                                          \
+    else                                                                                                           \
+      k_walk_scale<FO, WT, DI, false><<<grid, kBlock, 0, s>>>(g->d, P, L, walk_begin, walk_count, shuffle,         \
+                                                              out_dev, len_dev, C);                                \
+  } while (0)
   const bool wt = g->weighted != 0, di = g->directed != 0;
   if (first_order) {
     if (wt) GW_LAUNCH(true, true, false);

@@ -452,7 +452,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           const int j = upper_bound_i32(COx, sz + 1, c) - 1;
           const int k = c - COx[j];
           const int d = COx[j + 1] - COx[j];
-          const gw_ts_ent e = A.ent[Ol[j] + k];  // edges.get(j), insertion order (:103-110)
+          const gw_ts_ent e = gw_ts_load(A.ent + Ol[j] + k);  // edges.get(j), insertion order (:103-110)
           Vn[c] = e.x;
           Dn[c] = e.d;
           On[c] = e.off;
@@ -527,7 +527,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
               } else {
                 ux = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)t, 0u, A.k0, A.k1).x;
               }
-              const gw_ts_ent e = A.ent[ocur + gw_bounded(ux, (uint32_t)dcur)];  // randNeighbor
+              const gw_ts_ent e = gw_ts_load(A.ent + ocur + gw_bounded(ux, (uint32_t)dcur));  // randNeighbor
               path[t] = e.x;
               dpath[t] = e.d;
               dcur = e.d;
