@@ -25,7 +25,8 @@ constexpr int GW_BS_INLINE_BITS = 320;  // bitsets of deg(x) <= this live inside
 constexpr int GW_BS_LIST = 20;          // <= this many common neighbours: sorted u16 positions inline
 struct gw_bs_nbr {  // GW_N2V_BITSET: one 64 B entry (one HBM sector) per adjacency slot (u -> x)
   uint32_t x, d;                 // neighbour, deg(x)
-  uint32_t off_lo, off_hi;       // offsets[x]
+  uint32_t off;                  // offsets[x] (this mode needs < 2^32 adjacency entries)
+  uint32_t meta;                 // payload mode | Elias-Fano l << 2 | U << 7 | region dir blocks << 16
   uint32_t kp, c;                // position of u in N(x), #common neighbours
   uint32_t w[10];                // payload, by (c, d): c <= 20 && d < 65536: positions of the
                                  // common neighbours (u16, ascending, 0xFFFF padded); else

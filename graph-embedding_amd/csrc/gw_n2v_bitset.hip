@@ -110,6 +110,19 @@ __device__ __forceinline__ int bs_mode(uint32_t c, uint32_t d) {
   return gw_bs_is_list(c, d) ? BS_LIST : d <= (uint32_t)GW_BS_INLINE_BITS ? BS_INLINE : gw_bs_is_ef(c, d) ? BS_EF : BS_REGION;
 }
 
+// per-entry constants of the step kernel (no divisions per step):
+// mode | Elias-Fano l << 2 | U << 7 | directory blocks before the bits << 16
+__device__ __forceinline__ uint32_t bs_meta(uint32_t c, uint32_t d) {
+  const uint32_t mode = (uint32_t)bs_mode(c, d);
+  uint32_t l = 0, U = 0;
+  if (mode == BS_EF) {
+    l = (uint32_t)gw_bs_ef_l(c, d);
+    U = c + ((d - 1) >> l) + 1;
+  }
+  const uint32_t bblk = (mode == BS_REGION) ? (uint32_t)(bs_boff(d) / kBlk) : 0u;
+  return mode | (l << 2) | (U << 7) | (bblk << 16);
+}
+
 // first index in [b, e) with nbrs[i] >= key
 __device__ __forceinline__ int64_t lower_bound_i32(const int32_t* __restrict__ a, int64_t b, int64_t e, int32_t key) {
   while (b < e) {
@@ -298,7 +311,7 @@ __global__ void k_bs_count(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn, int64_t*
   else
     big[atomicAdd(nbig, 1ull)] = e;
   gw_bs_nbr* en = bsn + e;
-  *reinterpret_cast<uint4*>(en) = make_uint4((uint32_t)v, (uint32_t)d, (uint32_t)(uint64_t)vb, (uint32_t)((uint64_t)vb >> 32));
+  *reinterpret_cast<uint4*>(en) = make_uint4((uint32_t)v, (uint32_t)d, (uint32_t)(uint64_t)vb, 0u);
   *reinterpret_cast<uint2*>(&en->kp) = make_uint2(kp >= 0 ? (uint32_t)(kp - vb) : 0xFFFFFFFFu, c);
 }
 
@@ -335,8 +348,8 @@ __global__ void k_bs_fill_small(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn) {
   en.kp = 0xFFFFFFFFu;
   en.c = 0;
   en.d = (uint32_t)d;
-  en.off_lo = (uint32_t)(uint64_t)vb;
-  en.off_hi = (uint32_t)((uint64_t)vb >> 32);
+  en.off = (uint32_t)vb;
+  en.meta = 0;
 #pragma unroll
   for (int t = 0; t < 10; ++t) en.w[t] = 0;
   const int32_t u = row_of_slot(G.offsets, G.n, e);
@@ -352,6 +365,7 @@ __global__ void k_bs_fill_small(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn) {
     }
   }
   en.c = c;
+  en.meta = bs_meta(c, (uint32_t)d);
   if (gw_bs_is_list(c, (uint32_t)d)) {  // sorted positions, 0xFFFF padded
     uint16_t* lp = reinterpret_cast<uint16_t*>(en.w);
     for (int t = 0; t < 2 * 10; ++t) lp[t] = 0xFFFFu;
@@ -375,6 +389,7 @@ __global__ void k_bs_fill_thread(gw_dev_graph G, const uint64_t* __restrict__ ro
   if (min(S.ue - S.ub, d) > kThreadMin) return;  // k_bs_fill_wave
   gw_bs_nbr* en = bsn + e;
   const uint32_t c = en->c;
+  en->meta = bs_meta(c, (uint32_t)d);
   const BsEmit E = bs_emit(en, reg, roff, e, c, (uint32_t)d);
   if (E.mode == BS_LIST) {
     for (uint32_t t = c; t < 2 * 10; ++t) reinterpret_cast<uint16_t*>(en->w)[t] = 0xFFFFu;
@@ -404,6 +419,7 @@ __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff
     const BsEmit E = bs_emit(en, reg, roff, e, c, d);
     if (E.mode == BS_LIST && lane >= (int)c && lane < 2 * 10) reinterpret_cast<uint16_t*>(en->w)[lane] = 0xFFFFu;
     if (E.mode == BS_REGION && lane == 0) en->w[0] = (uint32_t)(roff[e] / kBlk);
+    if (lane == 0) en->meta = bs_meta(c, d);
     int64_t klast;
     common_wave(G, bs_slot(G, e), E, &klast);
     if (E.mode == BS_REGION)
@@ -549,6 +565,17 @@ __device__ __forceinline__ bool ef_has(const uint32_t (&pl)[10], uint32_t c, uin
   return false;
 }
 
+// Elias-Fano membership of k (high part h) once bucket h's first bit s is
+// known: the ones from s on are bucket h's elements, indices q - h
+__device__ __forceinline__ bool ef_scan(const uint32_t (&pl)[10], uint32_t U, int l, uint32_t h, uint32_t s, uint32_t k) {
+  const uint32_t lowk = k & ((1u << l) - 1u);
+  for (uint32_t q = s; q < U; ++q) {
+    if (!((pick10(pl, q >> 5) >> (q & 31)) & 1u)) break;
+    if (ef_low(pl, U, q - h, l) == lowk) return true;
+  }
+  return false;
+}
+
 // k in the inline common-neighbour list (registers, constant indices)
 __device__ __forceinline__ bool list_has(const uint32_t (&pl)[10], uint32_t k) {
   bool hit = false;
@@ -617,8 +644,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
     b = (uint32_t)G.offsets[cur];
     d = (uint32_t)(G.offsets[cur + 1] - G.offsets[cur]);
   }
-  uint32_t c = 0, kp = 0, boff = 0;
-  bool inl = true, lst = false, efm = false;
+  uint32_t c = 0, kp = 0, meta = 0;
   uint32_t pl[10];  // entry payload
 #pragma unroll
   for (int t = 0; t < 10; ++t) pl[t] = 0xFFFFFFFFu;
@@ -627,47 +653,131 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
     if (__ballot(active) == 0ull) break;
     uint32_t slot = 0xFFFFFFFFu;  // entry to fetch (accepted step)
     if (active) {
-      const uint32_t* h = G.bs_region + (uint64_t)pl[0] * kBlk;  // region mode only
-      int64_t k;
+      const uint32_t mode = meta & 3u;
+      const int efl = (int)((meta >> 2) & 31u);
+      const uint32_t efU = (meta >> 7) & 511u;
+      int64_t k = 0;
       bool acc = true;
-      const int efl = efm ? gw_bs_ef_l(c, d) : 0;  // Elias-Fano low bits and bit count
-      const uint32_t efU = efm ? c + ((d - 1) >> efl) + 1 : 0u;
       const gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
       ++trial;
+      // op 1: the j-th common position (select); op 2: is draw k common (membership)
+      int op = 0;
+      uint32_t j = 0;
       if (len == 1) {
-        k = (int64_t)gw_bounded(u.x, (uint32_t)d);
-      } else if (trial == 1) {
-        const double Z = (P.a_p + (double)c) + (double)((int64_t)d - 1 - (int64_t)c) * P.a_q;
-        const double r = gw_u01(u.x) * Z;
-        if (r < P.a_p) {
-          k = kp;  // return to prev
-        } else if (r - P.a_p < (double)c) {
-          uint32_t j = (uint32_t)(r - P.a_p);
-          if (j >= c) j = c - 1;
-          k = (P.diag & 1) ? (int64_t)((uint64_t)j * (uint64_t)d / c)
-              : lst        ? (int64_t)((pick10(pl, j >> 1) >> (16 * (j & 1))) & 0xFFFFu)
-              : inl        ? (int64_t)regs_select<10>(pl, j)
-              : efm        ? ef_select(pl, efU, efl, j)
-                           : bs_select(pl, h, (int64_t)d, c, j);
-        } else {
-          k = (int64_t)gw_bounded(u.y, (uint32_t)d);
-          const uint32_t fb = gw_bounded(u.y, kFilt);
-          const bool common = (P.diag & 2) ? false
-                              : lst ? list_has(pl, (uint32_t)k)
-                              : inl ? ((pick10(pl, (uint32_t)(k >> 5)) >> (k & 31)) & 1u)
-                              : efm ? ef_has(pl, c, efU, efl, (uint32_t)k)
-                              : ((pick10(pl, 5 + (fb >> 5)) >> (fb & 31)) & 1u) && ((h[boff + (k >> 5)] >> (k & 31)) & 1u);
-          acc = (k != (int64_t)kp) && !common;
+        k = (int64_t)gw_bounded(u.x, d);
+      } else {
+        bool other = trial > 1;  // a retry is always the "other" branch
+        if (!other) {
+          const double Z = (P.a_p + (double)c) + (double)((int64_t)d - 1 - (int64_t)c) * P.a_q;
+          const double r = gw_u01(u.x) * Z;
+          if (r < P.a_p) {
+            k = kp;  // return to prev
+          } else if (r - P.a_p < (double)c) {
+            j = (uint32_t)(r - P.a_p);
+            if (j >= c) j = c - 1;
+            op = 1;
+          } else {
+            other = true;
+          }
         }
-      } else {  // retry of the "other" branch
-        k = (int64_t)gw_bounded(u.y, (uint32_t)d);
-        const uint32_t fb = gw_bounded(u.y, kFilt);
-        const bool common = lst ? list_has(pl, (uint32_t)k)
-                            : inl ? ((pick10(pl, (uint32_t)(k >> 5)) >> (k & 31)) & 1u)
-                            : efm ? ef_has(pl, c, efU, efl, (uint32_t)k)
-                            : ((pick10(pl, 5 + (fb >> 5)) >> (fb & 31)) & 1u) && ((h[boff + (k >> 5)] >> (k & 31)) & 1u);
-        acc = ((k != (int64_t)kp) && !common) || trial >= (1u << 24);
+        if (other) {
+          k = (int64_t)gw_bounded(u.y, d);
+          op = 2;
+        }
       }
+      if (P.diag) {  // timing experiments only
+        if (op == 1 && (P.diag & 1)) {
+          k = (int64_t)((uint64_t)j * (uint64_t)d / c);
+          op = 0;
+        }
+        if (op == 2 && (P.diag & 2)) {
+          acc = k != (int64_t)kp;
+          op = 0;
+        }
+      }
+      // One shared select per trial: the t-th set bit of 16 words that are
+      // the payload (inline bitset, Elias-Fano high parts), its complement
+      // (Elias-Fano bucket start), or a 64 B region block.
+      bool sel = false, inv = false, mem = false;
+      uint32_t t = 0, gblk = 0;  // target rank; region block (global 64 B block index)
+      int64_t g = 0;             // region: block within the row
+      uint32_t eh = 0;           // Elias-Fano membership: high part of k
+      bool common = false;
+      if (op == 1) {
+        if (mode == BS_LIST) {
+          k = (int64_t)((pick10(pl, j >> 1) >> (16 * (j & 1))) & 0xFFFFu);
+        } else if (mode != BS_REGION) {
+          sel = true;
+          t = j;
+        } else {
+          const int64_t ndir = bs_ndir(d);
+          uint32_t jj = j;
+          if (ndir > kPDir) {
+            const uint32_t* h = G.bs_region + (uint64_t)pl[0] * kBlk;
+            g = dir_block([&](int64_t x) { return h[x]; }, ndir, c, &jj);
+          } else if (ndir > 0) {  // directory of <= 8 u16 counts in w[1..4]: count entries <= j
+            uint32_t lo = 0;
+#pragma unroll
+            for (int q = 1; q < kPDir; ++q) {
+              const uint32_t dq = (pl[1 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
+              const bool in = q < ndir && dq <= j;
+              g += in ? 1 : 0;
+              lo = in ? dq : lo;
+            }
+            jj = j - lo;
+          }
+          sel = mem = true;
+          t = jj;
+          gblk = pl[0] + (meta >> 16) + (uint32_t)g;
+        }
+      } else if (op == 2) {
+        if (mode == BS_LIST) {
+          common = list_has(pl, (uint32_t)k);
+        } else if (mode == BS_INLINE) {
+          common = (pick10(pl, (uint32_t)(k >> 5)) >> (k & 31)) & 1u;
+        } else if (mode == BS_EF) {
+          eh = (uint32_t)k >> efl;
+          if (eh > 0 && eh <= efU - c) {
+            sel = inv = true;
+            t = eh - 1;
+          }
+        } else {
+          const uint32_t fb = gw_bounded(u.y, kFilt);
+          if ((pick10(pl, 5 + (fb >> 5)) >> (fb & 31)) & 1u) {
+            const uint32_t* h = G.bs_region + ((uint64_t)pl[0] + (meta >> 16)) * kBlk;
+            common = (h[k >> 5] >> (k & 31)) & 1u;
+          }
+        }
+      }
+      if (sel) {
+        uint32_t wd[kBlk];
+        if (mem) {
+          const uint4* blk = reinterpret_cast<const uint4*>(G.bs_region) + (uint64_t)gblk * 4u;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint4 v = blk[q];
+            wd[4 * q] = v.x;
+            wd[4 * q + 1] = v.y;
+            wd[4 * q + 2] = v.z;
+            wd[4 * q + 3] = v.w;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < kBlk; ++q) wd[q] = q < 10 ? (inv ? ~pl[q] : pl[q]) : 0u;
+        }
+        const int pos = regs_select<kBlk>(wd, t);
+        if (op == 1) {
+          k = mode == BS_INLINE ? (int64_t)pos
+              : mode == BS_EF   ? (((int64_t)(uint32_t)(pos - (int)j) << efl) | ef_low(pl, efU, j, efl))
+                                : g * kDirBits + pos;
+        } else {  // Elias-Fano bucket eh starts after the (eh-1)-th zero
+          common = ef_scan(pl, efU, efl, eh, (uint32_t)pos + 1u, (uint32_t)k);
+        }
+      } else if (op == 2 && mode == BS_EF && eh == 0) {
+        common = ef_scan(pl, efU, efl, 0u, 0u, (uint32_t)k);
+      }
+      if (op == 2) acc = (k != (int64_t)kp) && !common;
+      if (trial >= (1u << 24)) acc = true;
       if (acc) {
         my_trials += trial;
         trial = 0;
@@ -687,6 +797,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
         cur = (int32_t)e0.x;
         d = e0.y;
         b = e0.z;
+        meta = e0.w;
         kp = e1.x;
         c = e1.y;
         pl[0] = e1.z; pl[1] = e1.w; pl[2] = e2.x; pl[3] = e2.y; pl[4] = e2.z;
@@ -695,11 +806,6 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
       __builtin_amdgcn_wave_barrier();
     }
     if (slot != 0xFFFFFFFFu) {
-      lst = gw_bs_is_list(c, (uint32_t)d);
-      inl = !lst && d <= (uint32_t)GW_BS_INLINE_BITS;
-      efm = gw_bs_is_ef(c, d);
-      boff = (uint32_t)bs_boff(d);
-
       stage[64 * (len & (kStage - 1))] = cur;
       if ((len & (kStage - 1)) == kStage - 1) {
         int32_t* dst = out + i * (int64_t)L + (len - (kStage - 1));
