@@ -49,7 +49,8 @@ constexpr int kSmallD = 32;      // thread-per-slot fill up to this degree
 constexpr int kStage = 16;
 
 constexpr int kPDir = 8;         // region entries with <= this many directory blocks keep the directory in the entry
-constexpr uint32_t kFilt = 160;  // coarse filter buckets in a region entry (w[5..9])
+constexpr uint32_t kFilt = 160;  // coarse filter buckets in a region entry (w[5..9]) ...
+constexpr uint32_t kFiltW = 288; // ... or w[1..9] when the entry holds no directory (d <= 512 or d > 4096)
 
 __host__ __device__ __forceinline__ int64_t bs_ndir(int64_t d) { return d > kDirBits ? (d + kDirBits - 1) / kDirBits : 0; }
 __host__ __device__ __forceinline__ int64_t bs_round(int64_t w) { return (w + kBlk - 1) / kBlk * kBlk; }
@@ -81,6 +82,10 @@ __device__ __forceinline__ bool bs_has_edge(const gw_dev_graph& G, int64_t rb, i
   }
   return gw_row_find(G.nbrs, rb, re, key) >= 0;
 }
+
+// region entries: the draw filter's bucket count and first payload word
+__host__ __device__ __forceinline__ uint32_t bs_filt_buckets(int64_t ndir) { return (ndir > 0 && ndir <= kPDir) ? kFilt : kFiltW; }
+__host__ __device__ __forceinline__ uint32_t bs_filt_word(int64_t ndir) { return (ndir > 0 && ndir <= kPDir) ? 5u : 1u; }
 
 // position of the j-th (0-based) set bit of x (j < popc(x))
 __device__ __forceinline__ int word_select(uint32_t x, uint32_t j) {
@@ -252,8 +257,9 @@ struct BsEmit {
       // filter: the draws u with floor(u*d / 2^32) == k span at most two buckets
       const uint64_t ulo = (((uint64_t)k << 32) + d - 1) / d;
       const uint64_t uhi = ((((uint64_t)k + 1) << 32) + d - 1) / d - 1;
-      const uint32_t b0 = gw_bounded((uint32_t)ulo, kFilt), b1 = gw_bounded((uint32_t)uhi, kFilt);
-      for (uint32_t b = b0; b <= b1; ++b) atomicOr(&w[5 + (b >> 5)], 1u << (b & 31));
+      const uint32_t F = bs_filt_buckets(ndir), w0 = bs_filt_word(ndir);
+      const uint32_t b0 = gw_bounded((uint32_t)ulo, F), b1 = gw_bounded((uint32_t)uhi, F);
+      for (uint32_t b = b0; b <= b1; ++b) atomicOr(&w[w0 + (b >> 5)], 1u << (b & 31));
     }
   }
   // directory blocks [g0, g1] start after `count` common positions
@@ -587,16 +593,19 @@ __device__ __forceinline__ bool list_has(const uint32_t (&pl)[10], uint32_t k) {
 struct BsParams {
   double a_p, a_q;
   uint32_t k0, k1, pk0, pk1;
-  uint32_t diag;  // timing experiments only (GW_DIAG_BS): 1 = no select, 2 = no membership test
+  uint32_t diag;  // timing experiments only (GW_DIAG_BS): 1 = no select, 2 = no membership test,
+                 // 4 = region blocks / 8 = region words read from a small hot area (wrong walks)
 };
 
 // round j of a cooperative entry load: lane l fetches 16 B piece (l & 3) of
 // the entry of the walker in lane 16 j + (l >> 2) (none if that walker
 // fetches nothing)
-__device__ __forceinline__ uint4 coop_piece(const uint4* __restrict__ ents, uint32_t slot, int lane, int j) {
-  const uint32_t sj = (uint32_t)__shfl((int)slot, 16 * j + (lane >> 2), 64);
+__device__ __forceinline__ uint4 coop_piece(uint64_t sec, int lane, int j) {
+  const int src = 16 * j + (lane >> 2);
+  const uint64_t sj = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(sec >> 32), src, 64) << 32) |
+                      (uint32_t)__shfl((int)(uint32_t)sec, src, 64);
   uint4 r = make_uint4(0u, 0u, 0u, 0u);
-  if (sj != 0xFFFFFFFFu) r = ents[(uint64_t)sj * 4u + (uint32_t)(lane & 3)];
+  if (sj != 0ull) r = reinterpret_cast<const uint4*>(sj)[lane & 3];
   return r;
 }
 
@@ -608,7 +617,7 @@ __device__ __forceinline__ uint4 coop_piece(const uint4* __restrict__ ents, uint
 // of walker 16j+m's entry, and the pieces reach their walker through a 1 KB
 // per-wave LDS exchange.  The walk loop is therefore wave-uniform (lanes
 // whose walk is done idle in it until every lane of the wave is done).
-__global__ void __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(8, 8)))
+__global__ void __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(5, 5)))
 k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t walk_count, int shuffle,
               int32_t* __restrict__ out, int32_t* __restrict__ lens, unsigned long long* __restrict__ counters) {
   __shared__ int32_t s_stage[kB / 64][kStage][64];
@@ -648,149 +657,184 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
   uint32_t pl[10];  // entry payload
 #pragma unroll
   for (int t = 0; t < 10; ++t) pl[t] = 0xFFFFFFFFu;
+  // Region reads are pipelined with the entry loads: every loop iteration is
+  // ONE memory round trip for the wave.  A step that selects inside a region
+  // spends extra iterations (directory words, then the 64 B block: state
+  // ph = 1, 2, data carried in wd) while the other lanes keep stepping; a
+  // region membership test reads its bitset word together with the entry of
+  // the candidate (speculatively; dropped when the candidate is common).
+  uint32_t ph = 0, t = 0;  // phase; select rank (ph 1: j; ph 2: rank inside block g)
+  int64_t g = 0;           // region block within the row
+  uint32_t wd[kBlk];       // ph 1: directory entries g, g+1; ph 2: the block
+#pragma unroll
+  for (int q = 0; q < kBlk; ++q) wd[q] = 0u;
   for (;;) {
     const bool active = len < L && d != 0;
     if (__ballot(active) == 0ull) break;
-    uint32_t slot = 0xFFFFFFFFu;  // entry to fetch (accepted step)
+    uint32_t slot = 0xFFFFFFFFu;  // entry to fetch (accepted or speculative step)
+    bool spec = false;            // slot is accepted unless bit sbit of sw is set
+    uint32_t sw = 0u, sbit = 0u;
+    uint64_t sec = 0ull;  // 64 B sector this lane fetches: its next entry or a region block
+    bool isblk = false;
     if (active) {
       const uint32_t mode = meta & 3u;
       const int efl = (int)((meta >> 2) & 31u);
       const uint32_t efU = (meta >> 7) & 511u;
+      const uint32_t* hreg = G.bs_region + (uint64_t)pl[0] * kBlk;  // region mode only
+      const int64_t ndir = bs_ndir(d);
       int64_t k = 0;
-      bool acc = true;
-      const gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
-      ++trial;
-      // op 1: the j-th common position (select); op 2: is draw k common (membership)
-      int op = 0;
-      uint32_t j = 0;
-      if (len == 1) {
-        k = (int64_t)gw_bounded(u.x, d);
+      bool acc = false;
+      if (ph == 2) {  // the region block has arrived
+        k = g * kDirBits + regs_select<kBlk>(wd, t);
+        acc = true;
+        ph = 0;
+      } else if (ph == 1) {  // directory entries g, g+1 have arrived
+        const uint32_t lo = wd[0], hi = g + 1 < ndir ? wd[1] : c;
+        if (t < lo || t >= hi) {
+          g += t < lo ? -1 : 1;
+          wd[0] = hreg[g];
+          wd[1] = g + 1 < ndir ? hreg[g + 1] : 0u;
+        } else {
+          t -= lo;
+          ph = 2;
+        }
       } else {
-        bool other = trial > 1;  // a retry is always the "other" branch
-        if (!other) {
-          const double Z = (P.a_p + (double)c) + (double)((int64_t)d - 1 - (int64_t)c) * P.a_q;
-          const double r = gw_u01(u.x) * Z;
-          if (r < P.a_p) {
-            k = kp;  // return to prev
-          } else if (r - P.a_p < (double)c) {
-            j = (uint32_t)(r - P.a_p);
-            if (j >= c) j = c - 1;
-            op = 1;
-          } else {
-            other = true;
-          }
-        }
-        if (other) {
-          k = (int64_t)gw_bounded(u.y, d);
-          op = 2;
-        }
-      }
-      if (P.diag) {  // timing experiments only
-        if (op == 1 && (P.diag & 1)) {
-          k = (int64_t)((uint64_t)j * (uint64_t)d / c);
-          op = 0;
-        }
-        if (op == 2 && (P.diag & 2)) {
-          acc = k != (int64_t)kp;
-          op = 0;
-        }
-      }
-      // One shared select per trial: the t-th set bit of 16 words that are
-      // the payload (inline bitset, Elias-Fano high parts), its complement
-      // (Elias-Fano bucket start), or a 64 B region block.
-      bool sel = false, inv = false, mem = false;
-      uint32_t t = 0, gblk = 0;  // target rank; region block (global 64 B block index)
-      int64_t g = 0;             // region: block within the row
-      uint32_t eh = 0;           // Elias-Fano membership: high part of k
-      bool common = false;
-      if (op == 1) {
-        if (mode == BS_LIST) {
-          k = (int64_t)((pick10(pl, j >> 1) >> (16 * (j & 1))) & 0xFFFFu);
-        } else if (mode != BS_REGION) {
-          sel = true;
-          t = j;
+        const gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
+        ++trial;
+        int op = 0;  // 1: the j-th common position; 2: is draw k common
+        uint32_t j = 0;
+        if (len == 1) {
+          k = (int64_t)gw_bounded(u.x, d);
+          acc = true;
         } else {
-          const int64_t ndir = bs_ndir(d);
-          uint32_t jj = j;
-          if (ndir > kPDir) {
-            const uint32_t* h = G.bs_region + (uint64_t)pl[0] * kBlk;
-            g = dir_block([&](int64_t x) { return h[x]; }, ndir, c, &jj);
-          } else if (ndir > 0) {  // directory of <= 8 u16 counts in w[1..4]: count entries <= j
-            uint32_t lo = 0;
-#pragma unroll
-            for (int q = 1; q < kPDir; ++q) {
-              const uint32_t dq = (pl[1 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
-              const bool in = q < ndir && dq <= j;
-              g += in ? 1 : 0;
-              lo = in ? dq : lo;
+          bool other = trial > 1;  // a retry is always the "other" branch
+          if (!other) {
+            const double Z = (P.a_p + (double)c) + (double)((int64_t)d - 1 - (int64_t)c) * P.a_q;
+            const double r = gw_u01(u.x) * Z;
+            if (r < P.a_p) {
+              k = kp;  // return to prev
+              acc = true;
+            } else if (r - P.a_p < (double)c) {
+              j = (uint32_t)(r - P.a_p);
+              if (j >= c) j = c - 1;
+              op = 1;
+            } else {
+              other = true;
             }
-            jj = j - lo;
           }
-          sel = mem = true;
-          t = jj;
-          gblk = pl[0] + (meta >> 16) + (uint32_t)g;
-        }
-      } else if (op == 2) {
-        if (mode == BS_LIST) {
-          common = list_has(pl, (uint32_t)k);
-        } else if (mode == BS_INLINE) {
-          common = (pick10(pl, (uint32_t)(k >> 5)) >> (k & 31)) & 1u;
-        } else if (mode == BS_EF) {
-          eh = (uint32_t)k >> efl;
-          if (eh > 0 && eh <= efU - c) {
-            sel = inv = true;
-            t = eh - 1;
-          }
-        } else {
-          const uint32_t fb = gw_bounded(u.y, kFilt);
-          if ((pick10(pl, 5 + (fb >> 5)) >> (fb & 31)) & 1u) {
-            const uint32_t* h = G.bs_region + ((uint64_t)pl[0] + (meta >> 16)) * kBlk;
-            common = (h[k >> 5] >> (k & 31)) & 1u;
+          if (other) {
+            k = (int64_t)gw_bounded(u.y, d);
+            op = 2;
           }
         }
-      }
-      if (sel) {
-        uint32_t wd[kBlk];
-        if (mem) {
-          const uint4* blk = reinterpret_cast<const uint4*>(G.bs_region) + (uint64_t)gblk * 4u;
+        if (P.diag) {  // timing experiments only
+          if (op == 1 && (P.diag & 1)) {
+            k = (int64_t)((uint64_t)j * (uint64_t)d / c);
+            acc = true;
+            op = 0;
+          }
+          if (op == 2 && (P.diag & 2)) {
+            acc = k != (int64_t)kp;
+            op = 0;
+          }
+        }
+        bool common = false;
+        // payload selects: the j-th one (inline bitset, Elias-Fano high
+        // parts) or the (eh-1)-th zero (start of Elias-Fano bucket eh)
+        const uint32_t eh = (uint32_t)k >> efl;
+        const bool ef_mem = op == 2 && mode == BS_EF && eh <= efU - c;
+        if ((op == 1 && (mode == BS_INLINE || mode == BS_EF)) || (ef_mem && eh > 0)) {
+          const bool inv = op == 2;
+          uint32_t wp[10];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint4 v = blk[q];
-            wd[4 * q] = v.x;
-            wd[4 * q + 1] = v.y;
-            wd[4 * q + 2] = v.z;
-            wd[4 * q + 3] = v.w;
+          for (int q = 0; q < 10; ++q) wp[q] = inv ? ~pl[q] : pl[q];
+          const int pos = regs_select<10>(wp, inv ? eh - 1 : j);
+          if (op == 1) {
+            k = mode == BS_INLINE ? (int64_t)pos
+                                  : (((int64_t)(uint32_t)(pos - (int)j) << efl) | ef_low(pl, efU, j, efl));
+            acc = true;
+          } else {
+            common = ef_scan(pl, efU, efl, eh, (uint32_t)pos + 1u, (uint32_t)k);
           }
-        } else {
-#pragma unroll
-          for (int q = 0; q < kBlk; ++q) wd[q] = q < 10 ? (inv ? ~pl[q] : pl[q]) : 0u;
+        } else if (ef_mem) {
+          common = ef_scan(pl, efU, efl, 0u, 0u, (uint32_t)k);
         }
-        const int pos = regs_select<kBlk>(wd, t);
         if (op == 1) {
-          k = mode == BS_INLINE ? (int64_t)pos
-              : mode == BS_EF   ? (((int64_t)(uint32_t)(pos - (int)j) << efl) | ef_low(pl, efU, j, efl))
-                                : g * kDirBits + pos;
-        } else {  // Elias-Fano bucket eh starts after the (eh-1)-th zero
-          common = ef_scan(pl, efU, efl, eh, (uint32_t)pos + 1u, (uint32_t)k);
+          if (mode == BS_LIST) {
+            k = (int64_t)((pick10(pl, j >> 1) >> (16 * (j & 1))) & 0xFFFFu);
+            acc = true;
+          } else if (mode == BS_REGION) {
+            if (ndir > kPDir) {  // directory in the region: guess the block, verify next iteration
+              g = (int64_t)((float)j * (float)ndir / (float)c);
+              if (g >= ndir) g = ndir - 1;
+              wd[0] = hreg[g];
+              wd[1] = g + 1 < ndir ? hreg[g + 1] : 0u;
+              t = j;
+              ph = 1;
+            } else {  // <= 8 directory counts (u16) in w[1..4]: count those <= j
+              uint32_t lo = 0;
+              g = 0;
+#pragma unroll
+              for (int q = 1; q < kPDir; ++q) {
+                const uint32_t dq = (pl[1 + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu;
+                const bool in = q < ndir && dq <= j;
+                g += in ? 1 : 0;
+                lo = in ? dq : lo;
+              }
+              t = j - lo;
+              ph = 2;
+            }
+          }
+        } else if (op == 2) {
+          if (mode == BS_LIST) {
+            common = list_has(pl, (uint32_t)k);
+          } else if (mode == BS_INLINE) {
+            common = (pick10(pl, (uint32_t)(k >> 5)) >> (k & 31)) & 1u;
+          } else if (mode == BS_REGION && k != (int64_t)kp && trial < (1u << 24)) {
+            const uint32_t fb = gw_bounded(u.y, bs_filt_buckets(ndir));
+            if ((pick10(pl, bs_filt_word(ndir) + (fb >> 5)) >> (fb & 31)) & 1u) {  // maybe common: read the word
+              sw = (P.diag & 8) ? G.bs_region[((uint32_t)k >> 5) & 0xFFFFu]  // timing experiment: no TLB misses
+                                : hreg[(meta >> 16) * kBlk + (k >> 5)];
+              sbit = (uint32_t)(k & 31);
+              spec = true;
+            }
+          }
+          acc = (k != (int64_t)kp && !common) || trial >= (1u << 24);
         }
-      } else if (op == 2 && mode == BS_EF && eh == 0) {
-        common = ef_scan(pl, efU, efl, 0u, 0u, (uint32_t)k);
       }
-      if (op == 2) acc = (k != (int64_t)kp) && !common;
-      if (trial >= (1u << 24)) acc = true;
+      if (ph == 2 && !acc) {  // fetch the region block (this iteration's round trip)
+        sec = (P.diag & 4) ? (uint64_t)(G.bs_region + kBlk * ((pl[0] + (uint32_t)g) & 0xFFFu))
+                           : (uint64_t)(hreg + ((meta >> 16) + (uint32_t)g) * kBlk);
+        isblk = true;
+      }
       if (acc) {
-        my_trials += trial;
-        trial = 0;
         slot = b + (uint32_t)k;
+        sec = (uint64_t)(ents + (uint64_t)slot * 4u);
       }
     }
-    // cooperative entry load: all four rounds in flight, then the exchange
-    const uint4 r0 = coop_piece(ents, slot, lane, 0), r1 = coop_piece(ents, slot, lane, 1);
-    const uint4 r2 = coop_piece(ents, slot, lane, 2), r3 = coop_piece(ents, slot, lane, 3);
+    // cooperative sector load (entries and region blocks alike): all four
+    // rounds in flight, then the exchange
+    const uint4 r0 = coop_piece(sec, lane, 0), r1 = coop_piece(sec, lane, 1);
+    const uint4 r2 = coop_piece(sec, lane, 2), r3 = coop_piece(sec, lane, 3);
+    if (spec && ((sw >> sbit) & 1u)) {  // the candidate was common: rejected
+      slot = 0xFFFFFFFFu;
+      sec = 0ull;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       ex[lane] = j == 0 ? r0 : j == 1 ? r1 : j == 2 ? r2 : r3;
       __builtin_amdgcn_wave_barrier();
+      if ((lane >> 4) == j && isblk) {
+        const uint4* q = ex + 4 * (lane & 15);
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+          const uint4 v = q[z];
+          wd[4 * z] = v.x;
+          wd[4 * z + 1] = v.y;
+          wd[4 * z + 2] = v.z;
+          wd[4 * z + 3] = v.w;
+        }
+      }
       if ((lane >> 4) == j && slot != 0xFFFFFFFFu) {
         const uint4* q = ex + 4 * (lane & 15);
         const uint4 e0 = q[0], e1 = q[1], e2 = q[2], e3 = q[3];
@@ -804,6 +848,10 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
         pl[5] = e2.w; pl[6] = e3.x; pl[7] = e3.y; pl[8] = e3.z; pl[9] = e3.w;
       }
       __builtin_amdgcn_wave_barrier();
+    }
+    if (slot != 0xFFFFFFFFu) {
+      my_trials += trial;
+      trial = 0;
     }
     if (slot != 0xFFFFFFFFu) {
       stage[64 * (len & (kStage - 1))] = cur;
