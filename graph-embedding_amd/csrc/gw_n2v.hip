@@ -589,14 +589,15 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
   const bool fo = (p == 1.0 && q == 1.0);
   const char* nosent = getenv("GW_DIAG_NO_SENT");  // diagnostic A/B knob only
   if ((mode == GW_N2V_REJECTION || fo) && g->nnz && !(nosent && nosent[0] == '1')) {
-    // slot entries (16 B per slot) spare the candidate's offsets[] read.  Measured: +10% at
-    // R-MAT-20 (0.5 GB of entries), -6% at R-MAT-24 ef 6 (3.2 GB: 4x the footprint of nbrs[]
-    // on hot hub rows, while offsets[] stays cache resident), so only up to 1 GiB.
-    // First-order walks (p = q = 1) read nothing but the slot: one random
-    // 16 B read per step instead of nbrs[] then offsets[] (any size that fits).
+    // slot entries (16 B per slot, one dwordx4 per step) spare the candidate's
+    // offsets[] read: +14% on R-MAT-24 ef 16 (p=1, q=0.5; 8.3 GB of entries),
+    // so they are built whenever they fit in half of the free HBM
+    // (GW_SENT_MAX_GB caps them, an A/B knob).
     size_t fr = 0, tot = 0;
     const int64_t ent_bytes = g->nnz * (int64_t)sizeof(gw_ts_ent);
-    if ((fo || ent_bytes <= ((int64_t)1 << 30)) && hipMemGetInfo(&fr, &tot) == hipSuccess && (int64_t)fr / 2 > ent_bytes) {
+    int64_t ent_max = INT64_MAX;
+    if (const char* sm = getenv("GW_SENT_MAX_GB")) ent_max = (int64_t)(atof(sm) * (double)(1 << 30));
+    if (ent_bytes <= ent_max && hipMemGetInfo(&fr, &tot) == hipSuccess && (int64_t)fr / 2 > ent_bytes) {
       if (dev_alloc(g, &d.sent, g->nnz) == GW_OK) {
         k_scale_ent<<<grid_for(g->nnz), kBlock>>>(d, d.sent);
         GW_HIP_TRY(hipGetLastError());
