@@ -19,7 +19,8 @@
 //   deg      int32[n]     row lengths (TopSim reads deg(mid), deg(target))
 //   node_J/q int32/f64[nnz] per-node alias tables (weighted or REPLAY)
 //   edge_off int64[nnz+1], edge_J/q per-edge alias tables (REPLAY only)
-//   bitmap   u32[16*nnz/32] has_edge membership pre-filter (REJECTION, p/q != 1)
+//   bitmap   u32[16*nnz/32] has_edge membership pre-filter (BITSET build; REJECTION when eh does not fit)
+//   eh       int32[2*nnz] per-row open-addressing neighbour sets (REJECTION, p/q != 1)
 //   bs_*     per-edge common-neighbour bitsets (BITSET mode, sum(deg^2) bits)
 constexpr int GW_BS_INLINE_BITS = 320;  // bitsets of deg(x) <= this live inside the entry
 constexpr int GW_BS_LIST = 20;          // <= this many common neighbours: sorted u16 positions inline
@@ -69,6 +70,7 @@ struct gw_dev_graph {
   int32_t* edge_J = nullptr;
   double* edge_q = nullptr;
   uint32_t* bitmap = nullptr;  // has_edge pre-filter, 16 bits per entry
+  int32_t* eh = nullptr;       // REJECTION mode: exact has_edge hash, 2*deg(v) int32 slots per row at 2*offsets[v]
   uint32_t* bs_region = nullptr;  // GW_N2V_BITSET per-edge regions (gw_n2v_bitset.hip)
   gw_bs_nbr* bs_nbr = nullptr;    // [nnz] neighbour + region offset
   gw_ts_ent* sent = nullptr;      // [nnz] REJECTION mode: {x, deg(x), offsets[x]} per slot

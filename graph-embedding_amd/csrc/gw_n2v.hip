@@ -226,8 +226,29 @@ __device__ __forceinline__ uint64_t gw_bm_bit(int64_t rowb, int64_t deg, int32_t
   return 16ull * (uint64_t)rowb + (((uint64_t)h * (uint64_t)(16 * deg)) >> 32);
 }
 
+// Exact neighbour sets for has_edge: row r owns 2*deg(r) int32 slots at
+// 2*offsets[r] (load factor 1/2, linear probing from a multiply-shift hash);
+// a query reads one slot run, almost always inside one 64 B sector, instead
+// of the bitmap line plus a log2(deg)-probe binary search.
+__device__ __forceinline__ uint32_t gw_eh_slot(int32_t key, uint32_t cap) {
+  return (uint32_t)(((uint64_t)((uint32_t)key * 0x9E3779B1u) * (uint64_t)cap) >> 32);
+}
+
 __device__ __forceinline__ bool gw_has_edge(const gw_dev_graph& G, int64_t rb, int64_t re,
                                             int32_t key) {
+  if (G.eh) {
+    const uint32_t cap = (uint32_t)(2 * (re - rb));
+    if (cap == 0) return false;
+    const int32_t* __restrict__ t = G.eh + 2 * rb;
+    uint32_t s = gw_eh_slot(key, cap);
+    for (uint32_t i = 0; i < cap; ++i) {
+      const int32_t k = t[s];
+      if (k == key) return true;
+      if (k == -1) return false;
+      s = s + 1 == cap ? 0u : s + 1;
+    }
+    return false;
+  }
   if (G.bitmap) {
     const uint64_t bit = gw_bm_bit(rb, re - rb, key);
     if (!((G.bitmap[bit >> 5] >> (bit & 31)) & 1u)) return false;
@@ -244,6 +265,30 @@ __global__ void k_scale_ent(gw_dev_graph G, gw_ts_ent* __restrict__ ent) {
   v.off = G.offsets[x];
   v.d = (int32_t)(G.offsets[x + 1] - v.off);
   ent[e] = v;
+}
+
+// one thread per adjacency slot: insert nbrs[e] into its row's set
+__global__ void k_build_ehash(gw_dev_graph G, int32_t* __restrict__ eh) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= G.nnz) return;
+  int64_t lo = 0, hi = G.n;  // row of slot e
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (G.offsets[mid + 1] <= e)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  const int64_t rb = G.offsets[lo];
+  const uint32_t cap = (uint32_t)(2 * (G.offsets[lo + 1] - rb));
+  const int32_t key = G.nbrs[e];
+  int32_t* t = eh + 2 * rb;
+  uint32_t s = gw_eh_slot(key, cap);
+  for (uint32_t i = 0; i < cap; ++i) {
+    const int32_t old = atomicCAS(&t[s], -1, key);
+    if (old == -1 || old == key) return;
+    s = s + 1 == cap ? 0u : s + 1;
+  }
 }
 
 __global__ void k_build_bitmap(int64_t n, const int64_t* __restrict__ off,
@@ -449,6 +494,7 @@ void gw_dev_release(gw_graph* g) {
   dev_free(d.edge_J);
   dev_free(d.edge_q);
   dev_free(d.bitmap);
+  dev_free(d.eh);
   dev_free(d.sent);
   gw_dev_bitset_release(g);
   gw_dev_simrank_release(g);
@@ -573,10 +619,28 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
     g->edge_alias_entries = total;
   }
   dev_free(d.bitmap);
+  dev_free(d.eh);
   gw_dev_bitset_release(g);
   g->bitset_words = 0;
   const char* nobm = getenv("GW_DIAG_NO_BITMAP");  // diagnostic A/B knob only
-  if ((mode == GW_N2V_BITSET || (mode == GW_N2V_REJECTION && !(p == 1.0 && q == 1.0))) && g->nnz &&
+  const char* noeh = getenv("GW_DIAG_NO_EHASH");   // diagnostic A/B knob only
+  if (mode == GW_N2V_REJECTION && !(p == 1.0 && q == 1.0) && g->nnz && g->semantics == GW_SEM_NX_SIMPLE &&
+      !(noeh && noeh[0] == '1')) {
+    size_t fr = 0, tot = 0;
+    const int64_t slots = 2 * g->nnz;
+    if (slots < ((int64_t)1 << 32) && hipMemGetInfo(&fr, &tot) == hipSuccess && (int64_t)fr / 2 > slots * 4) {
+      if (dev_alloc(g, &d.eh, slots) == GW_OK) {
+        GW_HIP_TRY(hipMemset(d.eh, 0xFF, sizeof(int32_t) * (size_t)slots));
+        k_build_ehash<<<grid_for(g->nnz), kBlock>>>(d, d.eh);
+        GW_HIP_TRY(hipGetLastError());
+        GW_HIP_TRY(hipDeviceSynchronize());
+      } else {
+        d.eh = nullptr;
+        (void)hipGetLastError();
+      }
+    }
+  }
+  if ((mode == GW_N2V_BITSET || (mode == GW_N2V_REJECTION && !(p == 1.0 && q == 1.0) && !d.eh)) && g->nnz &&
       !(nobm && nobm[0] == '1')) {
     const int64_t words = (16 * g->nnz + 31) / 32 + 1;
     if ((rc = dev_alloc(g, &d.bitmap, words))) return rc;
