@@ -45,7 +45,7 @@ BYTES_PER_STEP = 36       # row bounds 16 + alias q/J 12 + nbr 4 + 
 TOPSIM_B_EXT = 52         # per path-extension
 TOPSIM_B_UPD = 24         # per pair-update
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
-RANDOM_LINE_PEAK = 4.8e10 # measured: random 4 B gathers, one per 128 B line, 8 GiB buffer (tools/calib)
+RANDOM_LINE_PEAK = 4.9e10 # measured: random 64 B sectors, one load instruction each, 8-32 GB tables (tools/calib/calib_sweep.hip)
 
 
 def parse():
@@ -71,6 +71,11 @@ def parse():
     ap.add_argument("--walk10m-edge-factor", type=int, default=6)
     ap.add_argument("--simrank-graph", default="blog", help="naive SimRank graph (blog or moreno)")
     ap.add_argument("--simrank-rounds", type=int, default=3, help="SimRank.java STEP")
+    ap.add_argument("--no-rmat24", action="store_true",
+                    help="skip config 4 (R-MAT-24 ef 16, p=1 q=0.5) on this GPU")
+    ap.add_argument("--secondary", choices=["auto", "all", "none"], default="auto",
+                    help="secondary workloads: auto = all at 1 GPU, none when ranks > 1 (scaling runs time "
+                         "the headline only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--topsim-sample", type=int, default=10000)
@@ -168,6 +173,8 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.secondary == "none" or (args.secondary == "auto" and world > 1):
+        args.no_topsim = args.no_walk10m = args.no_simrank = args.no_rmat24 = True
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -427,11 +434,13 @@ def main():
         }
 
     # ---- north_star: walks on a ~10M-node / ~100M-edge power-law graph ----
-    def run_walk10m(BG, build_s, wp, wq):
+    def run_walk10m(BG, build_s, wp, wq, scale, ef, what="north_star 10M/100M graph", force_rejection=False):
         bi = BG.info()
         t0 = time.perf_counter()
         bmode = "bitset"
         try:
+            if force_rejection:
+                raise C.CapacityError(C.GW_ERR_CAPACITY, "rejection requested")
             C.check(C.lib().gw_n2v_prepare(BG.handle, wp, wq, C.N2V_BITSET), BG.handle)
         except C.CapacityError:
             bmode = "rejection"
@@ -496,10 +505,10 @@ def main():
                                                  "for this graph (sum(deg^2) entries); SURVEY §6 measured "
                                                  "4.1e4-3.7e5 walk-steps/s/core on small graphs"}
         del bout
-        return {"metric": "walk-steps/sec (node2vec, north_star 10M/100M graph)", "value": bsteps / sec,
+        return {"metric": f"walk-steps/sec (node2vec, {what})", "value": bsteps / sec,
                 "unit": "walk-steps/s",
-                "config": {"workload": f"node2vec p={wp} q={wq} on Graph500 R-MAT scale-{args.walk10m_scale} "
-                                       f"ef {args.walk10m_edge_factor} (n={bi.n}, adjacency entries={bi.nnz}), "
+                "config": {"workload": f"node2vec p={wp} q={wq} on Graph500 R-MAT scale-{scale} "
+                                       f"ef {ef} (n={bi.n}, adjacency entries={bi.nnz}), "
                                        f"walk_length={L}, 1 walk/node per rank",
                            "sampler": bmode},
                 "kernel_ms": kms, "host_build_s": build_s, "prepare_s": bprep, "sampler_tables_gb": bsampler_gb,
@@ -511,8 +520,20 @@ def main():
         build_s = time.perf_counter() - t0
         BG.to_device(dev.index)
         # the bench's p/q, then p=q=1 (the north_star graph walked first-order)
-        secondary["walk_10m"] = run_walk10m(BG, build_s, args.p, args.q)
-        secondary["walk_10m_p1q1"] = run_walk10m(BG, build_s, 1.0, 1.0)
+        sc, ef = args.walk10m_scale, args.walk10m_edge_factor
+        secondary["walk_10m"] = run_walk10m(BG, build_s, args.p, args.q, sc, ef)
+        secondary["walk_10m_p1q1"] = run_walk10m(BG, build_s, 1.0, 1.0, sc, ef)
+        BG.free()
+
+    if not args.no_rmat24:
+        # config 4 on one GPU: R-MAT-24 ef 16, p=1 q=0.5 (bitset tables would need ~390 GB:
+        # rejection sampler with slot entries and per-row neighbour hash sets)
+        t0 = time.perf_counter()
+        BG = gwamd.GWGraph.rmat(24, 16, 0.57, 0.19, 0.19, args.seed)
+        build_s = time.perf_counter() - t0
+        BG.to_device(dev.index)
+        secondary["walk_rmat24_p1q05"] = run_walk10m(BG, build_s, 1.0, 0.5, 24, 16, "config 4 R-MAT-24 ef 16",
+                                                     force_rejection=True)
         BG.free()
 
     if not args.no_simrank:
