@@ -309,3 +309,67 @@ def test_bitset_mixed_payload_modes_equal_oracle(gw, oracle, tmp_path, p, q):
     np.testing.assert_array_equal(lens.cpu().numpy(), rl)
     assert int(cnt[0]) == int(rc[0]) and int(cnt[1]) == int(rc[1])
     assert n == 2600
+
+
+def _hub_edgelist(path):
+    """A hub of degree 5,999 (> 4096: its regions keep the popcount directory
+    in memory, the select path that reads directory words first) over a
+    random graph of ~30 edges per vertex, so hub slots have many common
+    neighbours (region payloads) and the periphery has list / Elias-Fano ones."""
+    rng = np.random.default_rng(77)
+    n = 6000
+    E = {(0, v) for v in range(1, n)}
+    for u in range(1, n):
+        for v in rng.choice(np.arange(1, n), 15, replace=False):
+            if v != u:
+                E.add((min(u, int(v)), max(u, int(v))))
+    with open(path, "w") as f:
+        for a, b in sorted(E):
+            f.write(f"{a} {b}\n")
+
+
+@pytest.mark.parametrize("p,q", [(0.25, 4), (4, 0.25)])
+def test_bitset_directory_hub_equals_oracle(gw, oracle, tmp_path, p, q):
+    import torch
+    from gwamd import _lib as C
+    path = str(tmp_path / "hub.edgelist")
+    _hub_edgelist(path)
+    G = gw.GWGraph.from_edgelist(path, " ", "nx").to_device(0)
+    C.check(C.lib().gw_n2v_prepare(G.handle, float(p), float(q), C.N2V_BITSET), G.handle)
+    assert G.info().max_degree > 4096
+    L, begin, count = 30, 777, 4000
+    out = torch.empty((count, L), dtype=torch.int32, device="cuda")
+    lens = torch.empty(count, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    C.check(C.lib().gw_n2v_walks(G.handle, L, 11, begin, count, 1, C.ptr(out), C.ptr(lens), C.ptr(cnt), None),
+            G.handle)
+    torch.cuda.synchronize()
+    ref, rl, rc = oracle.walks_bitset(G.export_csr(), p, q, 11, L, begin, count, nthreads=8)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    np.testing.assert_array_equal(lens.cpu().numpy(), rl)
+    assert int(cnt[0]) == int(rc[0]) and int(cnt[1]) == int(rc[1])
+    assert (out.cpu().numpy() == 0).sum() > count // 8  # the hub (dense id 0) is visited often
+
+
+@pytest.mark.parametrize("p,q", [(1, 0.5), (0.25, 4), (1, 1)])
+def test_rejection_rmat_equals_oracle(gw, oracle, p, q):
+    """Rejection sampler (slot entries + per-row neighbour hash sets) and the
+    first-order kernel on a power-law graph with hubs, walk windows and
+    counters against the oracle."""
+    import torch
+    from gwamd import _lib as C
+    G = gw.GWGraph.rmat(14, 16, 0.57, 0.19, 0.19, 3).to_device(0)
+    C.check(C.lib().gw_n2v_prepare(G.handle, float(p), float(q), C.N2V_REJECTION), G.handle)
+    info = G.info()
+    assert info.sampler_bytes >= info.nnz * 16  # slot entries built
+    L, begin, count = 40, 3 * G.n + 5, 6000
+    out = torch.empty((count, L), dtype=torch.int32, device="cuda")
+    lens = torch.empty(count, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    C.check(C.lib().gw_n2v_walks(G.handle, L, 21, begin, count, 1, C.ptr(out), C.ptr(lens), C.ptr(cnt), None),
+            G.handle)
+    torch.cuda.synchronize()
+    ref, rl, rc = oracle.walks_scale(dict(G.export_csr(), weights=None), p, q, 21, L, begin, count, nthreads=8)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    np.testing.assert_array_equal(lens.cpu().numpy(), rl)
+    assert int(cnt[0]) == int(rc[0]) and int(cnt[1]) == int(rc[1])
