@@ -3,7 +3,7 @@
     python graph-embedding_amd/build.py [--force] [--verbose]
 
 Output: graph-embedding_amd/gwamd/libgraphwalk.so (git-ignored, travels to
-the GPU box with the repo snapshot).  No CMake: the product is five
+the GPU box with the repo snapshot).  No CMake: the product is a handful of
 translation units.
 """
 import argparse
@@ -22,7 +22,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("GW_OFFLOAD_ARCH", "gfx950")
 
 HIP_SRCS = ["gw_n2v.hip", "gw_n2v_bitset.hip", "gw_topsim.hip", "gw_simrank.hip", "gw_topsim_m.hip", "gw_topsim_d.hip"]
-CXX_SRCS = ["gw_graph_host.cpp", "gw_capi.cpp"]
+CXX_SRCS = ["gw_graph_host.cpp", "gw_capi.cpp", "gw_comm.cpp"]
 HEADERS = ["gw_internal.h", "gw_philox.h", "gw_device_common.h"]
 
 HIPCC_FLAGS = [
@@ -34,7 +34,7 @@ HIPCC_FLAGS = [
 ]
 CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-fopenmp", "-ffp-contract=off",
              "-Wall", "-Wno-unused-function", f"-I{os.path.join(ROOT, 'include')}",
-             f"-I{ROCM}/include"]
+             f"-I{ROCM}/include", "-D__HIP_PLATFORM_AMD__"]
 
 
 def _newer(obj, deps):
@@ -77,7 +77,7 @@ def build(force=False, verbose=False):
         list(ex.map(lambda c: _run(c, verbose), jobs))
     if force or jobs or _newer(OUT, objs):
         _run([cxx, "-shared", "-o", OUT] + objs +
-             [f"-L{ROCM}/lib", "-lamdhip64", "-fopenmp", f"-Wl,-rpath,{ROCM}/lib",
+             [f"-L{ROCM}/lib", "-lamdhip64", "-fopenmp", "-ldl", f"-Wl,-rpath,{ROCM}/lib",
               "-Wl,--no-undefined"], verbose)
     # C++ host mirror of the Java TopSim API + the benchmark driver binary
     host = os.path.join(HERE, "host")

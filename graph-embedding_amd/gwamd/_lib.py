@@ -130,6 +130,11 @@ SIGNATURES = {
     "gw_write_sim_text_dense": (ctypes.c_int, [CP, P, P, I64, I64, ctypes.c_int, CP, ctypes.c_int]),
     "gw_write_sim_text_topk": (ctypes.c_int, [CP, P, P, P, I64, ctypes.c_int, CP, ctypes.c_int]),
     "gw_write_sim_text_cachemap": (ctypes.c_int, [CP, P, P, P, P, I64, ctypes.c_int, ctypes.c_int, CP]),
+    "gw_comm_unique_id": (ctypes.c_int, [P]),
+    "gw_comm_init": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, PP]),
+    "gw_comm_allgather": (ctypes.c_int, [P, P, P, I64, ctypes.c_int, P]),
+    "gw_comm_free": (ctypes.c_int, [P]),
+    "gw_comm_last_error": (CP, [P]),
 }
 
 _lib = None

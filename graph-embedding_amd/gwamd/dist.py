@@ -55,3 +55,45 @@ def allgather_rows(local, world, group=None):
         dist.all_gather(chunks, local.contiguous(), group=group)
     parts = [out[r * mx:r * mx + sizes[r]] for r in range(world)]
     return torch.cat(parts)
+
+
+class NativeComm:
+    """The C ABI's RCCL communicator (include/graphwalk.h gw_comm_*): the same
+    all-gather for hosts that do not run torch.distributed (JNI, C++ drivers).
+    Rank 0 creates the id with NativeComm.unique_id() and distributes it."""
+
+    def __init__(self, uid, nranks, rank, device):
+        import ctypes
+        from . import _lib as C
+        self._C = C
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        h = ctypes.c_void_p()
+        rc = C.lib().gw_comm_init(ctypes.cast(buf, ctypes.c_void_p), nranks, rank, device, ctypes.byref(h))
+        if rc != C.GW_OK:
+            raise C.DeviceError(rc, C.lib().gw_comm_last_error(None).decode(errors="replace"))
+        self.handle, self.nranks, self.rank = h, nranks, rank
+
+    @staticmethod
+    def unique_id():
+        import ctypes
+        from . import _lib as C
+        buf = (ctypes.c_uint8 * 128)()
+        rc = C.lib().gw_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p))
+        if rc != C.GW_OK:
+            raise C.DeviceError(rc, C.lib().gw_comm_last_error(None).decode(errors="replace"))
+        return bytes(buf)
+
+    def allgather(self, send, recv, stream=None):
+        """recv[nranks * n] = every rank's send[n] in rank order (int32 or float64 CUDA tensors)."""
+        C = self._C
+        dt = {torch.int32: 0, torch.float64: 1}[send.dtype]
+        assert recv.dtype == send.dtype and recv.numel() == self.nranks * send.numel()
+        st = None if stream is None else C.ctypes.c_void_p(stream.cuda_stream)
+        rc = C.lib().gw_comm_allgather(self.handle, C.ptr(send), C.ptr(recv), send.numel(), dt, st)
+        if rc != C.GW_OK:
+            raise C.DeviceError(rc, C.lib().gw_comm_last_error(self.handle).decode(errors="replace"))
+
+    def close(self):
+        if self.handle:
+            self._C.lib().gw_comm_free(self.handle)
+            self.handle = None

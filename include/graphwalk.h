@@ -327,6 +327,26 @@ int gw_write_sim_text_cachemap(const char* path, const int32_t* keys,
                                const int32_t* row_ids, int64_t nrows,
                                int capacity, int topk, const char* sep);
 
+/* ---- multi-GPU exchange (RCCL over xGMI) ---------------------------------- */
+/* the graph is replicated and units (walks, TopSim sources) are
+ * sharded by global index with no data-path collective; the only exchange is
+ * an all-gather of emitted blocks for hosts that need every walk on every
+ * rank.  One process (or thread) per GPU; RCCL (librccl.so.1) is loaded on
+ * first use, so the library itself carries no link-time RCCL dependency.
+ * Rank 0 calls gw_comm_unique_id and hands the GW_COMM_ID_BYTES bytes to the
+ * other ranks out of band (MPI, a file, torch.distributed, ...).            */
+#define GW_COMM_ID_BYTES 128
+#define GW_DTYPE_I32 0
+#define GW_DTYPE_F64 1
+typedef struct gw_comm gw_comm;
+int gw_comm_unique_id(uint8_t* id);
+int gw_comm_init(const uint8_t* id, int nranks, int rank, int device, gw_comm** out);
+/* recv_dev[nranks * count] = concatenation of every rank's send_dev[count]
+ * in rank order (ncclAllGather); asynchronous on `stream` (NULL = default). */
+int gw_comm_allgather(gw_comm* c, const void* send_dev, void* recv_dev, int64_t count, int dtype, void* stream);
+int gw_comm_free(gw_comm* c);
+const char* gw_comm_last_error(const gw_comm* c);
+
 #ifdef __cplusplus
 }
 #endif

@@ -373,3 +373,22 @@ def test_rejection_rmat_equals_oracle(gw, oracle, p, q):
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
     np.testing.assert_array_equal(lens.cpu().numpy(), rl)
     assert int(cnt[0]) == int(rc[0]) and int(cnt[1]) == int(rc[1])
+
+
+def test_native_comm_single_rank_allgather(gw):
+    """gw_comm (RCCL loaded at run time): a one-rank communicator gathers
+    int32 walk blocks and float64 score blocks unchanged."""
+    import torch
+    from gwamd import dist
+    c = dist.NativeComm(dist.NativeComm.unique_id(), 1, 0, 0)
+    try:
+        w = torch.arange(12345, dtype=torch.int32, device="cuda")
+        r = torch.empty_like(w)
+        c.allgather(w, r, torch.cuda.current_stream())
+        s = torch.rand(777, dtype=torch.float64, device="cuda")
+        rs = torch.empty_like(s)
+        c.allgather(s, rs)
+        torch.cuda.synchronize()
+        assert torch.equal(w, r) and torch.equal(s, rs)
+    finally:
+        c.close()
