@@ -14,3 +14,8 @@ timeout -k 10 600 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum --k
 python tools/kt_summary.py gpurun_out/prof_$TAG/kt_kernel_trace.csv gpurun_out/prof_$TAG/kernel_dispatch_summary.json > /dev/null
 echo ALL_OK
 find gpurun_out -name "*.csv" | head -20
+# TopSim on the 10M-vertex graph (config 5): kernel trace of that workload alone
+if [ -n "$P10M" ]; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_p10m_$TAG -o kt -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-simrank --no-walk10m --no-rmat24 --topsim-graphs p10m > gpurun_out/prof_p10m_$TAG.json 2> gpurun_out/prof_p10m_$TAG.err || { echo P10M_FAIL; tail -20 gpurun_out/prof_p10m_$TAG.err; exit 1; }
+  echo P10M_OK
+fi
