@@ -288,7 +288,7 @@ def main():
                      "lines_per_step": prof["fabric_read_requests_per_launch"] / max(launch_steps, 1)}
 
     # ---- parity spot check (cheap): every step follows an edge ----
-    if rank == 0 and not os.environ.get("GW_DIAG_BS"):  # (diagnostic timing knobs give wrong walks)
+    if rank == 0 and not (os.environ.get("GW_DIAG_BS") or os.environ.get("GW_DIAG_NO_STORE")):  # (diag knobs: wrong walks)
         csr = G.export_csr()
         smp = out[:2000].cpu().numpy()
         offs, nbrs = csr["offsets"], csr["nbrs"]

@@ -206,6 +206,7 @@ struct N2VParams {
   double h_prev;     // min(1/p, M): in-envelope height of the return edge
   uint32_t k0, k1;   // step key
   uint32_t pk0, pk1; // permutation key
+  uint32_t diag;     // timing experiments only (GW_DIAG_NO_STORE=1: no walk output stores)
 };
 
 template <bool WEIGHTED>
@@ -324,30 +325,41 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
   const int lane = threadIdx.x & 63;
   int32_t* stage = &s_stage[threadIdx.x >> 6][0][lane];  // slot j at stage[64*j]
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = i < walk_count;
   unsigned long long my_steps = 0, my_trials = 0;
-  if (i < walk_count) {
-    const int64_t w = walk_begin + i;
+  const int64_t w = walk_begin + (valid ? i : 0);
+  int32_t cur = -1;
+  int32_t prev = -1;
+  int64_t pb = 0, pe = 0;  // prev row bounds (undirected has_edge probes)
+  double w_back = 1.0;     // weight of edge cur<->prev (outlier area)
+  bool back_ok = false;    // cur -> prev exists (always true undirected)
+  const bool vec_ok = (L & 3) == 0;
+  int len = L;  // lanes past walk_count take no step
+  uint32_t trial = 0;
+  const uint32_t c0 = (uint32_t)w, c1 = (uint32_t)((uint64_t)w >> 32);
+  int64_t b = 0, e = 0;
+  int64_t nb = 0;  // candidate's row (slot entries)
+  int32_t nd = 0;
+  double Wcur = 0.0;
+  if (valid) {
     const uint64_t it = (uint64_t)w / (uint64_t)G.n;
     const uint64_t pos = (uint64_t)w % (uint64_t)G.n;
     const uint64_t sp = shuffle ? gw_feistel_perm(pos, (uint64_t)G.n, P.pk0, P.pk1, (uint32_t)it) : pos;
-    int32_t cur = G.order[sp];
-    int32_t prev = -1;
-    int64_t pb = 0, pe = 0;  // prev row bounds (undirected has_edge probes)
-    double w_back = 1.0;     // weight of edge cur<->prev (outlier area)
-    bool back_ok = false;    // cur -> prev exists (always true undirected)
-    int32_t* row = out + i * (int64_t)L;
-    const bool vec_ok = (L & 3) == 0;
-    stage[0] = cur;
-    int len = 1;
-    uint32_t trial = 0;
-    const uint32_t c0 = (uint32_t)w, c1 = (uint32_t)((uint64_t)w >> 32);
-    int64_t b = G.offsets[cur], e = G.offsets[cur + 1];
-    int64_t nb = 0;  // candidate's row (slot entries)
-    int32_t nd = 0;
-    double Wcur = WEIGHTED ? G.wsum[cur] : (double)(e - b);
-    while (len < L) {
+    cur = G.order[sp];
+    len = 1;
+    b = G.offsets[cur];
+    e = G.offsets[cur + 1];
+    Wcur = WEIGHTED ? G.wsum[cur] : (double)(e - b);
+  }
+  stage[0] = cur;
+  // wave-uniform loop: the stage flush below is cooperative
+  for (;;) {
+    const bool active = len < L && e != b;  // e == b: directed sink (node2vec.py:36-37)
+    if (__ballot(active) == 0ull) break;
+    bool ready = false;  // this lane completed 16 staged positions (flen-15 .. flen)
+    int flen = 0;
+    if (active) {
       const int64_t d = e - b;
-      if (d == 0) break;  // directed sink (node2vec.py:36-37)
       bool acc;
       int64_t slot;
       int32_t next;
@@ -420,19 +432,8 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
         pe = e;
         cur = next;
         stage[64 * (len & (kStage - 1))] = cur;
-        if ((len & (kStage - 1)) == kStage - 1) {  // flush positions len-15 .. len
-          int32_t* dst = row + (len - (kStage - 1));
-          if (vec_ok) {
-#pragma unroll
-            for (int j = 0; j < kStage; j += 4) {
-              int4 v = make_int4(stage[64 * j], stage[64 * (j + 1)], stage[64 * (j + 2)], stage[64 * (j + 3)]);
-              *reinterpret_cast<int4*>(dst + j) = v;
-            }
-          } else {
-#pragma unroll
-            for (int j = 0; j < kStage; ++j) dst[j] = stage[64 * j];
-          }
-        }
+        ready = (len & (kStage - 1)) == kStage - 1;
+        flen = len;
         ++len;
         if (FIRST_ORDER && ENT) {
           b = nb;
@@ -453,7 +454,36 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
         else Wcur = (double)(e - b);
       }
     }
+    // flush: 64 contiguous bytes per ready walker.  Cooperative (like the
+    // bitset kernel's loads): in round j lanes 4m..4m+3 store the four 16 B
+    // pieces of walker 16j+m's chunk, so an instruction writes 16 whole
+    // sectors instead of a 16 B piece of 64 (per-lane stores cost up to 22%
+    // of a launch: GW_DIAG_NO_STORE A/B)
+    const unsigned long long rm = __ballot(ready);
+    if (rm && !P.diag) {
+      if (vec_ok) {
+        __builtin_amdgcn_wave_barrier();
+        const int32_t* sw = &s_stage[threadIdx.x >> 6][0][0];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 16 * j + (lane >> 2), p4 = 4 * (lane & 3);
+          const int lr = __shfl(flen, r, 64);
+          const int64_t ir = ((int64_t)__shfl((int)(i >> 32), r, 64) << 32) | (uint32_t)__shfl((int)i, r, 64);
+          if ((rm >> r) & 1ull) {
+            const int4 v = make_int4(sw[64 * p4 + r], sw[64 * (p4 + 1) + r], sw[64 * (p4 + 2) + r], sw[64 * (p4 + 3) + r]);
+            *reinterpret_cast<int4*>(out + ir * (int64_t)L + (lr - (kStage - 1)) + p4) = v;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      } else if (ready) {
+        int32_t* dst = out + i * (int64_t)L + (flen - (kStage - 1));
+        for (int j = 0; j < kStage; ++j) dst[j] = stage[64 * j];
+      }
+    }
+  }
+  if (valid) {
     // tail: staged positions [len & ~15, len) then -1 padding up to L
+    int32_t* row = out + i * (int64_t)L;
     const int base = len & ~(kStage - 1);
     for (int t = base; t < len; ++t) row[t] = stage[64 * (t - base)];
     for (int t = len; t < L; ++t) row[t] = -1;
@@ -833,6 +863,10 @@ int gw_dev_n2v_walks(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int6
   P.k1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_STEP;
   P.pk0 = (uint32_t)seed;
   P.pk1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_PERM;
+  {
+    const char* ns = getenv("GW_DIAG_NO_STORE");
+    P.diag = (ns && ns[0] == '1') ? 1u : 0u;
+  }
   if (g->n2v_mode == GW_N2V_BITSET && !first_order)
     return gw_dev_walk_bitset_launch(g, L, seed, walk_begin, walk_count, shuffle, out_dev, len_dev, counters_dev,
                                      stream);

@@ -853,21 +853,36 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
       my_trials += trial;
       trial = 0;
     }
+    bool ready = false;  // this lane completed 16 staged positions (flen-15 .. flen)
+    int flen = 0;
     if (slot != 0xFFFFFFFFu) {
       stage[64 * (len & (kStage - 1))] = cur;
-      if ((len & (kStage - 1)) == kStage - 1) {
-        int32_t* dst = out + i * (int64_t)L + (len - (kStage - 1));
-        if (vec_ok) {
-#pragma unroll
-          for (int j = 0; j < kStage; j += 4)
-            *reinterpret_cast<int4*>(dst + j) =
-                make_int4(stage[64 * j], stage[64 * (j + 1)], stage[64 * (j + 2)], stage[64 * (j + 3)]);
-        } else {
-#pragma unroll
-          for (int j = 0; j < kStage; ++j) dst[j] = stage[64 * j];
-        }
-      }
+      ready = (len & (kStage - 1)) == kStage - 1;
+      flen = len;
       ++len;
+    }
+    // flush of the ready walkers' 64 B chunks, cooperative like the loads:
+    // an instruction writes 16 whole sectors instead of a 16 B piece of 64
+    const unsigned long long rm = __ballot(ready);
+    if (rm && !(P.diag & 32)) {
+      if (vec_ok) {
+        __builtin_amdgcn_wave_barrier();
+        const int32_t* sw = &s_stage[wv][0][0];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 16 * j + (lane >> 2), p4 = 4 * (lane & 3);
+          const int lr = __shfl(flen, r, 64);
+          const int64_t ir = ((int64_t)__shfl((int)(i >> 32), r, 64) << 32) | (uint32_t)__shfl((int)i, r, 64);
+          if ((rm >> r) & 1ull) {
+            const int4 v = make_int4(sw[64 * p4 + r], sw[64 * (p4 + 1) + r], sw[64 * (p4 + 2) + r], sw[64 * (p4 + 3) + r]);
+            *reinterpret_cast<int4*>(out + ir * (int64_t)L + (lr - (kStage - 1)) + p4) = v;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      } else if (ready) {
+        int32_t* dst = out + i * (int64_t)L + (flen - (kStage - 1));
+        for (int j = 0; j < kStage; ++j) dst[j] = stage[64 * j];
+      }
     }
   }
   if (valid) {
@@ -1013,6 +1028,7 @@ int gw_dev_walk_bitset_launch(gw_graph* g, int L, uint64_t seed, int64_t walk_be
   P.pk1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_PERM;
   const char* dg = getenv("GW_DIAG_BS");  // diagnostic A/B knob only
   P.diag = dg ? (uint32_t)atoi(dg) : 0u;
+  if (const char* ns = getenv("GW_DIAG_NO_STORE")) P.diag |= ns[0] == '1' ? 32u : 0u;
   const unsigned grid = (unsigned)std::max<int64_t>(1, (walk_count + kB - 1) / kB);
   k_walk_bitset<<<grid, kB, 0, (hipStream_t)stream>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev,
                                                        len_dev, (unsigned long long*)counters_dev);
