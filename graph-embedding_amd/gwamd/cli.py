@@ -13,7 +13,16 @@ save_list format (DeepSim/src/main.py:237-243) or as .npy.
 
 --mode replay : reference-exact (networkx graph, global random/np.random
                 seeded with --seed, per-edge alias tables on the GPU);
---mode scale  : Philox/rejection kernel (any size; identical for any GPU count).
+--mode scale  : Philox samplers (any size; identical for any GPU count):
+                --sampler auto picks the per-edge bitset sampler when its
+                tables fit (unweighted undirected graphs), else rejection.
+
+Multi-GPU (scale mode): launch one process per GPU with torchrun; rank r
+walks its contiguous block of the global walk indices on GPU LOCAL_RANK, the
+blocks are all-gathered over RCCL (gwamd.dist.allgather_rows) and rank 0
+writes the file, identical to a one-GPU run.
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m gwamd.cli --mode scale ...
 """
 import argparse
 import random
@@ -46,6 +55,10 @@ def parse_args(argv=None, p=1.0, q=1.0):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--mode", choices=["replay", "scale"], default="replay")
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--sampler", choices=["auto", "bitset", "rejection"], default="auto",
+                    help="scale mode: second-order sampler")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="torch.distributed backend when launched with several ranks (nccl = RCCL)")
     return ap.parse_args(argv)
 
 
@@ -62,6 +75,66 @@ def read_graph(args):
     if not args.directed:
         G = G.to_undirected()
     return G
+
+
+def _scale(args):
+    """--mode scale on one GPU or, under torchrun, one block of walks per rank."""
+    import os
+    import torch
+    from . import _lib as C
+    from . import dist as gd
+    from . import io
+    from .graph import GWGraph
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    device = args.device
+    if world > 1:
+        import torch.distributed as dist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        device = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(args.dist_backend)
+    g = GWGraph.from_edgelist(args.input, args.delimiter, "nx", args.directed, args.weighted)
+    g.to_device(device)
+    mode = C.N2V_REJECTION
+    if args.sampler != "rejection" and not args.directed and not args.weighted and (args.p, args.q) != (1.0, 1.0):
+        try:
+            C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, C.N2V_BITSET), g.handle)
+            mode = C.N2V_BITSET
+        except C.CapacityError:
+            if args.sampler == "bitset":
+                raise
+    if mode == C.N2V_REJECTION:
+        C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, C.N2V_REJECTION), g.handle)
+    nwalks = args.num_walks * g.n
+    L = args.walk_length
+    begin, count = gd.shard_range(nwalks, world, rank)
+    W = torch.empty((count, L), dtype=torch.int32, device=f"cuda:{device}")
+    lens = torch.empty(count, dtype=torch.int32, device=f"cuda:{device}")
+    st = torch.cuda.current_stream(device)
+    C.check(C.lib().gw_n2v_walks(g.handle, L, args.seed, begin, count, 1, C.ptr(W), C.ptr(lens), None,
+                                 C.ctypes.c_void_p(st.cuda_stream)), g.handle)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        if args.dist_backend != "nccl":  # (gloo rehearsals gather host tensors)
+            W, lens = W.cpu(), lens.cpu()
+        W = gd.allgather_rows(W, world)
+        lens = gd.allgather_rows(lens.view(-1, 1), world).view(-1)
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+        if rank != 0:
+            return None
+    W, lens = W.cpu().numpy(), lens.cpu().numpy()
+    if args.walks.endswith(".npy"):
+        lab = g.export_csr()["labels"]
+        np.save(args.walks, np.where(W >= 0, lab[np.maximum(W, 0)], -1))
+    else:
+        io.save_walks(g, args.walks, W, lens)
+    return nwalks
 
 
 def main(argv=None):
@@ -85,22 +158,9 @@ def main(argv=None):
             io.save_list(walks, args.walks)
         nwalks = len(walks)
     else:
-        from . import _lib as C
-        from .graph import GWGraph
-        g = GWGraph.from_edgelist(args.input, args.delimiter, "nx", args.directed, args.weighted)
-        g.to_device(args.device)
-        C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, C.N2V_REJECTION), g.handle)
-        n = g.n
-        nwalks = args.num_walks * n
-        W = np.empty((nwalks, args.walk_length), np.int32)
-        lens = np.empty(nwalks, np.int32)
-        C.check(C.lib().gw_n2v_walks_host(g.handle, args.walk_length, args.seed, 0, nwalks, 1, C.ptr(W),
-                                          C.ptr(lens), None), g.handle)
-        if args.walks.endswith(".npy"):
-            lab = g.export_csr()["labels"]
-            np.save(args.walks, np.where(W >= 0, lab[np.maximum(W, 0)], -1))
-        else:
-            io.save_walks(g, args.walks, W, lens)
+        nwalks = _scale(args)
+        if nwalks is None:  # not rank 0
+            return 0
     print(f"{nwalks} walks -> {args.walks} in {time.time() - t0:.2f}s", file=sys.stderr)
     return 0
 

@@ -392,3 +392,29 @@ def test_native_comm_single_rank_allgather(gw):
         assert torch.equal(w, r) and torch.equal(s, rs)
     finally:
         c.close()
+
+
+def test_cli_scale_two_ranks_equal_one(gw, tmp_path):
+    """gwamd.cli --mode scale under torchrun: two ranks (gloo rehearsal on one
+    GPU; RCCL on a multi-GPU node) walk their blocks and rank 0 writes a file
+    byte-identical to the one-process run."""
+    import socket
+    import subprocess
+    import sys
+    from gwamd import cli
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "graph-embedding_amd")
+    common = ["--input", os.path.join(DATA, "moreno_crime_crime.txt"), "--delimiter", "\t", "--p", "0.25",
+              "--q", "4", "--seed", "3", "--mode", "scale", "--num-walks", "3", "--walk-length", "30"]
+    one = tmp_path / "one.txt"
+    assert cli.main(common + ["--walks", str(one)]) == 0
+    two = tmp_path / "two.txt"
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, PYTHONPATH=pkg + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "gwamd.cli"] + common +
+                       ["--walks", str(two), "--dist-backend", "gloo"], env=env, capture_output=True, text=True,
+                       timeout=150)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert one.read_bytes() == two.read_bytes()
