@@ -936,25 +936,65 @@ extern "C" int gw_n2v_walks_host(gw_graph* g, int walk_len, uint64_t seed, int64
     return gw_fail(g, GW_ERR_INVALID, "bad arguments");
   if (walk_count == 0) return GW_OK;
   GW_HIP_TRY(hipSetDevice(g->device));
-  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(walk_count, ((int64_t)1 << 30) / (4 * (int64_t)walk_len)));
-  int32_t *d_out = nullptr, *d_len = nullptr;
+  // Chunks of ~256 MB of walks, double-buffered: chunk k+1 is walked on one
+  // stream while chunk k is copied out on another (a pageable copy blocks
+  // the host, so the next kernel is enqueued before it).
+  int64_t chunk_bytes = (int64_t)256 << 20;
+  if (const char* cm = getenv("GW_HOST_CHUNK_MB")) chunk_bytes = std::max<int64_t>(1, atoll(cm)) << 20;
+  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(walk_count, chunk_bytes / (4 * (int64_t)walk_len)));
+  const int64_t nch = (walk_count + chunk - 1) / chunk;
+  int32_t *d_out[2] = {nullptr, nullptr}, *d_len[2] = {nullptr, nullptr};
   uint64_t* d_cnt = nullptr;
-  int rc;
-  if ((rc = dev_alloc(g, &d_out, chunk * (int64_t)walk_len)) || (rc = dev_alloc(g, &d_len, chunk)) ||
-      (rc = dev_alloc(g, &d_cnt, 2))) {
-    dev_free(d_out); dev_free(d_len); dev_free(d_cnt);
+  hipStream_t sc = nullptr, sx = nullptr;
+  hipEvent_t done[2] = {nullptr, nullptr};
+  auto release = [&]() {
+    for (int b = 0; b < 2; ++b) {
+      dev_free(d_out[b]);
+      dev_free(d_len[b]);
+      if (done[b]) (void)hipEventDestroy(done[b]);
+    }
+    dev_free(d_cnt);
+    if (sc) (void)hipStreamDestroy(sc);
+    if (sx) (void)hipStreamDestroy(sx);
+  };
+  int rc = GW_OK;
+  const int nb = nch > 1 ? 2 : 1;
+  for (int b = 0; b < nb && rc == GW_OK; ++b)
+    if ((rc = dev_alloc(g, &d_out[b], chunk * (int64_t)walk_len)) == GW_OK) rc = dev_alloc(g, &d_len[b], chunk);
+  if (rc == GW_OK) rc = dev_alloc(g, &d_cnt, 2);
+  if (rc != GW_OK) {
+    release();
     return rc;
   }
-  hipError_t e = hipMemset(d_cnt, 0, 2 * sizeof(uint64_t));
-  for (int64_t c0 = 0; c0 < walk_count && e == hipSuccess; c0 += chunk) {
-    const int64_t cn = std::min(chunk, walk_count - c0);
-    rc = gw_dev_n2v_walks(g, walk_len, seed, walk_begin + c0, cn, shuffle, d_out, d_len, d_cnt, nullptr);
-    if (rc != GW_OK) break;
-    e = hipMemcpy(out_walks + c0 * walk_len, d_out, cn * walk_len * sizeof(int32_t), hipMemcpyDeviceToHost);
-    if (e == hipSuccess && out_len) e = hipMemcpy(out_len + c0, d_len, cn * sizeof(int32_t), hipMemcpyDeviceToHost);
+  hipError_t e = hipStreamCreateWithFlags(&sc, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&sx, hipStreamNonBlocking);
+  for (int b = 0; b < nb && e == hipSuccess; ++b) e = hipEventCreateWithFlags(&done[b], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMemsetAsync(d_cnt, 0, 2 * sizeof(uint64_t), sc);
+  auto launch = [&](int64_t k) -> int {
+    const int64_t c0 = k * chunk, cn = std::min(chunk, walk_count - c0);
+    const int b = (int)(k & 1);
+    int r = gw_dev_n2v_walks(g, walk_len, seed, walk_begin + c0, cn, shuffle, d_out[b], d_len[b], d_cnt, sc);
+    if (r == GW_OK && hipEventRecord(done[b], sc) != hipSuccess) r = GW_ERR_DEVICE;
+    return r;
+  };
+  if (e == hipSuccess) rc = launch(0);
+  for (int64_t k = 0; k < nch && e == hipSuccess && rc == GW_OK; ++k) {
+    // buffer (k+1)&1 was last read by the copy of chunk k-1, finished below
+    if (k + 1 < nch && (rc = launch(k + 1)) != GW_OK) break;
+    const int64_t c0 = k * chunk, cn = std::min(chunk, walk_count - c0);
+    const int b = (int)(k & 1);
+    e = hipStreamWaitEvent(sx, done[b], 0);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(out_walks + c0 * walk_len, d_out[b], cn * walk_len * sizeof(int32_t),
+                         hipMemcpyDeviceToHost, sx);
+    if (e == hipSuccess && out_len)
+      e = hipMemcpyAsync(out_len + c0, d_len[b], cn * sizeof(int32_t), hipMemcpyDeviceToHost, sx);
+    if (e == hipSuccess) e = hipStreamSynchronize(sx);
   }
-  if (rc == GW_OK && e == hipSuccess && counters) e = hipMemcpy(counters, d_cnt, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost);
-  dev_free(d_out); dev_free(d_len); dev_free(d_cnt);
+  if (rc == GW_OK && e == hipSuccess) e = hipStreamSynchronize(sc);
+  if (rc == GW_OK && e == hipSuccess && counters)
+    e = hipMemcpy(counters, d_cnt, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  release();
   if (rc != GW_OK) return rc;
   if (e != hipSuccess) return gw_fail(g, GW_ERR_DEVICE, "%s", hipGetErrorString(e));
   return GW_OK;

@@ -418,3 +418,30 @@ def test_cli_scale_two_ranks_equal_one(gw, tmp_path):
                        timeout=150)
     assert r.returncode == 0, r.stderr[-2000:]
     assert one.read_bytes() == two.read_bytes()
+
+
+@pytest.mark.parametrize("mode", ["bitset", "rejection"])
+def test_walks_host_pipeline_equals_device(gw, mode, monkeypatch):
+    """gw_n2v_walks_host (chunked, kernel/copy overlapped on two streams):
+    identical walks, lengths and counters to one device-buffer call, with
+    small chunks so the double buffering wraps many times."""
+    import torch
+    from gwamd import _lib as C
+    G = gw.GWGraph.rmat(13, 16, 0.57, 0.19, 0.19, 5).to_device(0)
+    C.check(C.lib().gw_n2v_prepare(G.handle, 0.25, 4.0, C.N2V_BITSET if mode == "bitset" else C.N2V_REJECTION),
+            G.handle)
+    L, begin, count = 40, 1234, 30001
+    out = torch.empty((count, L), dtype=torch.int32, device="cuda")
+    lens = torch.empty(count, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    C.check(C.lib().gw_n2v_walks(G.handle, L, 9, begin, count, 1, C.ptr(out), C.ptr(lens), C.ptr(cnt), None),
+            G.handle)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("GW_HOST_CHUNK_MB", "1")  # 6,553 walks per chunk: 5 chunks
+    W = np.empty((count, L), np.int32)
+    ln = np.empty(count, np.int32)
+    hc = np.zeros(2, np.uint64)
+    C.check(C.lib().gw_n2v_walks_host(G.handle, L, 9, begin, count, 1, C.ptr(W), C.ptr(ln), C.ptr(hc)), G.handle)
+    np.testing.assert_array_equal(W, out.cpu().numpy())
+    np.testing.assert_array_equal(ln, lens.cpu().numpy())
+    assert int(hc[0]) == int(cnt[0]) and int(hc[1]) == int(cnt[1])
