@@ -490,37 +490,94 @@ int gw_rmat_java_impl(gw_graph* g, int64_t n, int64_t m, double a, double b, dou
 int gw_write_walks_impl(const gw_graph* g, const char* path, const int32_t* walks,
                         const int32_t* lens, int64_t nwalks, int walk_len,
                         std::string* err) {
+  // Every label's decimal text once (a flat table), then walks are formatted
+  // by copying those strings: chunks of walks in parallel, each into its own
+  // buffer, written in order and overlapped with formatting the next batch.
+  const int64_t n = g->n;
+  std::vector<uint64_t> loff((size_t)n + 1, 0);
+#pragma omp parallel for schedule(static)
+  for (int64_t v = 0; v < n; ++v) {
+    char tmp[32];
+    auto r = std::to_chars(tmp, tmp + sizeof tmp, (long long)g->labels[v]);
+    loff[v + 1] = (uint64_t)(r.ptr - tmp) + 1;  // + '\t'
+  }
+  for (int64_t v = 0; v < n; ++v) loff[v + 1] += loff[v];
+  std::vector<char> ltxt(loff[n]);
+#pragma omp parallel for schedule(static)
+  for (int64_t v = 0; v < n; ++v) {
+    auto r = std::to_chars(ltxt.data() + loff[v], ltxt.data() + loff[v + 1], (long long)g->labels[v]);
+    *r.ptr = '\t';
+  }
   FILE* f = fopen(path, "wb");
   if (!f) {
     *err = std::string("cannot open '") + path + "'";
     return GW_ERR_IO;
   }
-  const int64_t chunk = 1 << 14;
-  std::vector<std::string> bufs;
+  const int64_t chunk = 1 << 13;
+  const int64_t nchunks = (nwalks + chunk - 1) / chunk;
+  const int64_t batch = 256;  // chunks formatted per round
+  std::vector<std::vector<char>> buf[2];
   int rc = GW_OK;
-  for (int64_t c0 = 0; c0 < nwalks && rc == GW_OK; c0 += chunk * 64) {
-    int64_t c1 = std::min(nwalks, c0 + chunk * 64);
-    int64_t nb = (c1 - c0 + chunk - 1) / chunk;
-    bufs.assign(nb, std::string());
-#pragma omp parallel for schedule(dynamic)
-    for (int64_t bi = 0; bi < nb; ++bi) {
-      std::string& s = bufs[bi];
-      char tmp[32];
-      for (int64_t wi = c0 + bi * chunk; wi < std::min(c1, c0 + (bi + 1) * chunk); ++wi) {
-        const int32_t* w = walks + wi * (int64_t)walk_len;
-        int L = lens ? lens[wi] : walk_len;
-        for (int t = 0; t < L && w[t] >= 0; ++t) {
-          auto r = std::to_chars(tmp, tmp + sizeof tmp, (long long)g->labels[w[t]]);
-          s.append(tmp, r.ptr);
-          s.push_back('\t');
+  int bad = 0;
+  for (int64_t b0 = 0, round = 0; b0 < nchunks && rc == GW_OK; b0 += batch, ++round) {
+    auto& cur = buf[round & 1];
+    const int64_t nb = std::min(batch, nchunks - b0);
+    cur.resize((size_t)nb);
+    auto& prev = buf[(round + 1) & 1];
+    const int64_t nprev = round > 0 ? (int64_t)prev.size() : 0;
+#pragma omp parallel
+    {
+#pragma omp single nowait
+      {  // one thread writes the previous round while the others format this one
+        for (int64_t k = 0; k < nprev; ++k)
+          if (fwrite(prev[k].data(), 1, prev[k].size(), f) != prev[k].size()) rc = GW_ERR_IO;
+      }
+#pragma omp for schedule(dynamic)
+      for (int64_t bi = 0; bi < nb; ++bi) {
+        std::vector<char>& out = cur[bi];
+        const int64_t w0 = (b0 + bi) * chunk, w1 = std::min(nwalks, w0 + chunk);
+        size_t sz = 0;
+        for (int64_t wi = w0; wi < w1; ++wi) {
+          const int32_t* w = walks + wi * (int64_t)walk_len;
+          const int L = lens ? lens[wi] : walk_len;
+          for (int t = 0; t < L && w[t] >= 0; ++t) {
+            if (w[t] >= n) {
+              bad = 1;
+              break;
+            }
+            sz += loff[w[t] + 1] - loff[w[t]];
+          }
+          ++sz;
         }
-        s.push_back('\n');
+        out.resize(sz);
+        char* o = out.data();
+        for (int64_t wi = w0; wi < w1; ++wi) {
+          const int32_t* w = walks + wi * (int64_t)walk_len;
+          const int L = lens ? lens[wi] : walk_len;
+          for (int t = 0; t < L && w[t] >= 0 && w[t] < n; ++t) {
+            const uint64_t a = loff[w[t]], e = loff[w[t] + 1];
+            memcpy(o, ltxt.data() + a, e - a);
+            o += e - a;
+          }
+          *o++ = '\n';
+        }
+        out.resize((size_t)(o - out.data()));
       }
     }
-    for (auto& s : bufs)
-      if (fwrite(s.data(), 1, s.size(), f) != s.size()) rc = GW_ERR_IO;
+    prev.clear();
+    if (bad) break;
   }
-  if (fclose(f) != 0) rc = GW_ERR_IO;
+  if (!bad && rc == GW_OK) {
+    auto& last = buf[(((nchunks + batch - 1) / batch) - 1) & 1];
+    if (nchunks > 0)
+      for (auto& c : last)
+        if (fwrite(c.data(), 1, c.size(), f) != c.size()) rc = GW_ERR_IO;
+  }
+  if (fclose(f) != 0 && rc == GW_OK) rc = GW_ERR_IO;
+  if (bad) {
+    *err = "walk entry outside the graph";
+    return GW_ERR_RANGE;
+  }
   if (rc != GW_OK) *err = "write failed";
   return rc;
 }

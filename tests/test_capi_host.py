@@ -232,3 +232,24 @@ def test_cachemap_writer_format(gw, oracle, tmp_path):
         exp = [(int(keys[r, i]), float(vals[r, i])) for i in range(lo, size[r])]
         assert lines[r].decode() == f"{r}" + "".join(f",{k}:{oracle.java_format_fixed(v)}" for k, v in exp)
         assert ids[r].decode() == f"{r}" + "".join(f",{k}" for k, _ in exp)
+
+
+def test_walk_writer_large_and_range(gw, tmp_path):
+    """The parallel writer (label text table, chunked formatting overlapped
+    with ordered writes) equals Python's save_list across many chunks and
+    batches, and refuses entries outside the graph (GW_ERR_RANGE)."""
+    from gwamd import io
+    G = gw.GWGraph.rmat(10, 8, seed=7)
+    lab = G.export_csr()["labels"]
+    rng = np.random.default_rng(3)
+    nw, L = 2_100_000 // 20, 20  # 105,000 walks: 13 chunks of 8,192
+    W = rng.integers(0, G.n, (nw, L)).astype(np.int32)
+    cut = rng.integers(1, L + 1, nw)
+    W[np.arange(L)[None, :] >= cut[:, None]] = -1  # ragged walks, -1 padded
+    p1 = tmp_path / "a.txt"
+    io.save_walks(G, p1, W)
+    expect = "".join("".join(f"{int(lab[x])}\t" for x in row[row >= 0]) + "\n" for row in W)
+    assert p1.read_text() == expect
+    W[nw // 2, 0] = G.n  # outside the graph
+    with pytest.raises(IndexError):  # GW_ERR_RANGE
+        io.save_walks(G, tmp_path / "b.txt", W)
