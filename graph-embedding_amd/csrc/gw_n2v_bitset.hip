@@ -18,20 +18,29 @@
 //                              bitset: expected d/(d-1-c) ~ 1 trial)
 //
 // Per edge slot s = (u -> v):
-//   bs_nbr[s] (64 B, one HBM sector): v, d = deg(v), offsets[v] (int64),
-//            kp (position of u in N(v)), c, and a 40 B payload: the common
-//            positions (u16 list or Elias-Fano), the bitset itself (d <= 320),
-//            or for a region: w[0] = its 64 B block index, w[1..4] = the
-//            directory (u16 counts, d <= 4096), w[5..9] = a 160-bucket filter
-//            over the draw u (bucket = u*160 >> 32; bit set iff some u in the
-//            bucket lands on a common position), so most "other"-branch
-//            membership tests never read the region
+//   bs_nbr[s] (64 B, one HBM sector): v, d = deg(v), offsets[v] (u32: this
+//            mode needs < 2^32 slots), meta (payload mode, Elias-Fano l and U,
+//            directory blocks), kp (position of u in N(v)), c, and a 40 B
+//            payload: the common positions (u16 list or Elias-Fano), the
+//            bitset itself (d <= 320), or for a region: w[0] = its 64 B block
+//            index, w[1..4] = the directory (u16 counts, 512 < d <= 4096),
+//            then a draw filter over u (w[5..9]: 160 buckets, or w[1..9]: 288
+//            when the entry holds no directory; bucket = u*F >> 32, bit set
+//            iff some u in the bucket lands on a common position), so most
+//            "other"-branch membership tests never read the region
 //   region   (d > 320, payload full) dir[ndir]  cumulative set bits before
 //                       each 512-bit block (d > 4096 only), then
 //            bits[ceil(d/32)]  bit k = (N(v)[k] != u) && has_edge(N(v)[k], u)
 // The entry chosen by a step carries everything the next step needs, so a
 // step into a vertex of degree <= 320 touches ONE random sector (the entry);
-// larger degrees add the bitset word (~2 sectors, vs ~7 for rejection).
+// region selects and unfiltered membership tests add one (1.34 per step on
+// R-MAT-20, vs ~7 for rejection sampling with binary-search probes).
+//
+// Access shape (k_walk_bitset): entries and region blocks are fetched by a
+// cooperative load (16 walkers' sectors per instruction) through a per-wave
+// LDS exchange; region reads are pipelined so every loop iteration is one
+// round trip for the wave; finished 16-position chunks of the walks are
+// written by a cooperative flush.  See DESIGN.md §3.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
