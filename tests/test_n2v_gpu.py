@@ -445,3 +445,31 @@ def test_walks_host_pipeline_equals_device(gw, mode, monkeypatch):
     np.testing.assert_array_equal(W, out.cpu().numpy())
     np.testing.assert_array_equal(ln, lens.cpu().numpy())
     assert int(hc[0]) == int(cnt[0]) and int(hc[1]) == int(cnt[1])
+
+
+@pytest.mark.parametrize("mode,p,q", [("bitset", 0.25, 4), ("rejection", 1, 0.5), ("rejection", 1, 1)])
+def test_walk_shapes_edge_cases(gw, oracle, mode, p, q):
+    """Partial waves and blocks (1, 63, 65, 257 walks), walk lengths around
+    the 16-position flush (1, 15, 16, 17, 33) and zero walks: every sampler
+    equals the oracle, including the cooperative flush's tail handling."""
+    import torch
+    from gwamd import _lib as C
+    G = gw.GWGraph.from_edgelist(os.path.join(DATA, "moreno_crime_crime.txt"), "\t", "nx").to_device(0)
+    C.check(C.lib().gw_n2v_prepare(G.handle, float(p), float(q),
+                                   C.N2V_BITSET if mode == "bitset" else C.N2V_REJECTION), G.handle)
+    csr = G.export_csr()
+    C.check(C.lib().gw_n2v_walks(G.handle, 8, 1, 0, 0, 1, None, None, None, None), G.handle)  # no walks: no-op
+    for count in (1, 63, 65, 257):
+        for L in (1, 15, 16, 17, 33):
+            begin = 7 * count + L
+            out = torch.full((count, L), -7, dtype=torch.int32, device="cuda")
+            lens = torch.empty(count, dtype=torch.int32, device="cuda")
+            C.check(C.lib().gw_n2v_walks(G.handle, L, 13, begin, count, 1, C.ptr(out), C.ptr(lens), None, None),
+                    G.handle)
+            torch.cuda.synchronize()
+            if mode == "bitset":
+                ref, rl, _ = oracle.walks_bitset(csr, p, q, 13, L, begin, count, nthreads=4)
+            else:
+                ref, rl, _ = oracle.walks_scale(dict(csr, weights=None), p, q, 13, L, begin, count, nthreads=4)
+            np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"count={count} L={L}")
+            np.testing.assert_array_equal(lens.cpu().numpy(), rl)
