@@ -35,16 +35,16 @@ struct gw_bs_nbr {  // GW_N2V_BITSET: one 64 B entry (one HBM sector) per adjace
                                  // they fit in 320 bits; else w[0..1] = region word offset
 };
 #if defined(__HIPCC__)
-#define GW_HD __host__ __device__
+#define GW_BS_HD __host__ __device__
 #else
-#define GW_HD
+#define GW_BS_HD
 #endif
-GW_HD inline bool gw_bs_is_list(uint32_t c, uint32_t d) { return c <= GW_BS_LIST && d < 65536u; }
+GW_BS_HD inline bool gw_bs_is_list(uint32_t c, uint32_t d) { return c <= GW_BS_LIST && d < 65536u; }
 // Elias-Fano payload (neither list nor inline bitset): the unary high parts
 // (U = c + ((d-1)>>l) + 1 bits) first, then l low bits per position; fits
 // when U + c*l <= 320.  l = floor(log2(d / c)).
-GW_HD inline int gw_bs_ef_l(uint32_t c, uint32_t d) { return 31 - __builtin_clz(d / c); }
-GW_HD inline bool gw_bs_is_ef(uint32_t c, uint32_t d) {
+GW_BS_HD inline int gw_bs_ef_l(uint32_t c, uint32_t d) { return 31 - __builtin_clz(d / c); }
+GW_BS_HD inline bool gw_bs_is_ef(uint32_t c, uint32_t d) {
   if (gw_bs_is_list(c, d) || d <= (uint32_t)GW_BS_INLINE_BITS || c == 0) return false;
   const int l = gw_bs_ef_l(c, d);
   return (uint64_t)c * l + c + ((d - 1) >> l) + 1 <= (uint64_t)GW_BS_INLINE_BITS;  // U + c*l
