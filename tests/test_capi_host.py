@@ -253,3 +253,22 @@ def test_walk_writer_large_and_range(gw, tmp_path):
     W[nw // 2, 0] = G.n  # outside the graph
     with pytest.raises(IndexError):  # GW_ERR_RANGE
         io.save_walks(G, tmp_path / "b.txt", W)
+
+
+def test_comm_argument_errors(gw):
+    """gw_comm_* without a GPU: argument checks and error strings (RCCL is
+    loaded only on first use; no collective runs here)."""
+    import ctypes
+    from gwamd import _lib as C
+    L = gw.lib()
+    uid = (ctypes.c_uint8 * 128)()
+    h = ctypes.c_void_p()
+    p_uid = ctypes.cast(uid, ctypes.c_void_p)
+    assert L.gw_comm_init(p_uid, 2, 2, 0, ctypes.byref(h)) == C.GW_ERR_INVALID  # rank >= nranks
+    assert L.gw_comm_init(p_uid, 0, 0, 0, ctypes.byref(h)) == C.GW_ERR_INVALID
+    assert L.gw_comm_init(None, 1, 0, 0, ctypes.byref(h)) == C.GW_ERR_INVALID
+    assert L.gw_last_error(None) is not None
+    assert L.gw_comm_last_error(None) == b"bad arguments"
+    assert L.gw_comm_allgather(None, None, None, 4, 0, None) == C.GW_ERR_INVALID
+    assert L.gw_comm_free(None) == C.GW_OK
+    assert L.gw_comm_unique_id(None) == C.GW_ERR_INVALID
