@@ -1,5 +1,7 @@
 #!/bin/bash
-# bench + rocprofv3 kernel trace + PMC (FETCH_SIZE / WRITE_SIZE in separate passes)
+# bench + rocprofv3 kernel trace + PMC (FETCH_SIZE / WRITE_SIZE in separate passes).
+# kernel_dispatch_summary.json splits each kernel by grid size: the headline launch
+# (R-MAT-20, 6,463,230 walks) is the k_walk_bitset row with grid=6463232.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
