@@ -1,0 +1,144 @@
+"""Access model of k_walk_bitset: replays a sample of walks exactly (same
+Philox draws as the kernel and the oracle) and counts, per step, the random
+64 B sectors the kernel reads beyond the step's entry — region membership
+words the draw filter cannot answer, region selects (block, and directory
+words at hubs with d > 4096) — by payload mode and branch.  CPU only; the
+sum is compared with the measured fabric read requests per step
+(profiles/pmc_summary.json).
+
+    python tools/bitset_access_model.py [--scale 20] [--walks 600]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "graph-embedding_amd"))
+sys.path.insert(0, ROOT)
+
+M32 = 0xFFFFFFFF
+TAG_STEP = 0x6E327632  # GW_TAG_N2V_STEP
+
+
+def philox(c0, c1, c2, c3, k0, k1):
+    """Philox4x32-10 (csrc/gw_philox.h)."""
+    for _ in range(10):
+        p0 = 0xD2511F53 * c0
+        p1 = 0xCD9E8D57 * c2
+        hi0, lo0 = p0 >> 32, p0 & M32
+        hi1, lo1 = p1 >> 32, p1 & M32
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0) & M32, lo1, (hi0 ^ c3 ^ k1) & M32, lo0
+        k0 = (k0 + 0x9E3779B9) & M32
+        k1 = (k1 + 0xBB67AE85) & M32
+    return c0, c1, c2, c3
+
+
+def bounded(x, d):
+    return (x * d) >> 32
+
+
+def mode_of(c, d):
+    if c <= 20 and d < 65536:
+        return "list"
+    if d <= 320:
+        return "inline"
+    if c > 0:
+        l = int(np.floor(np.log2(d // c))) if d // c > 0 else 0
+        if c * l + c + ((d - 1) >> l) + 1 <= 320:
+            return "ef"
+    return "region"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=int, default=20)
+    ap.add_argument("--p", type=float, default=0.25)
+    ap.add_argument("--q", type=float, default=4.0)
+    ap.add_argument("--walks", type=int, default=600)
+    ap.add_argument("--seed", type=int, default=42)
+    a = ap.parse_args()
+    import gwamd
+    import oracle
+    G = gwamd.GWGraph.rmat(a.scale, 16, 0.57, 0.19, 0.19, 42)
+    csr = G.export_csr()
+    off, nbrs = csr["offsets"], csr["nbrs"]
+    n = len(off) - 1
+    L = 80
+    begin = 7 * n + 11  # a window inside the bench's first step
+    W, lens, _ = oracle.walks_bitset(csr, a.p, a.q, a.seed, L, begin, a.walks, nthreads=8)
+    ap_, aq = 1.0 / a.p, 1.0 / a.q
+    k0, k1 = a.seed & M32, ((a.seed >> 32) ^ TAG_STEP) & M32
+    cnt = {}
+    steps = 0
+
+    def add(key, v=1):
+        cnt[key] = cnt.get(key, 0) + v
+
+    for i in range(a.walks):
+        w = begin + i
+        c0, c1 = w & M32, (w >> 32) & M32
+        for t in range(2, int(lens[i])):
+            prev, cur = int(W[i, t - 2]), int(W[i, t - 1])
+            row = nbrs[off[cur]:off[cur + 1]]
+            d = len(row)
+            prow = nbrs[off[prev]:off[prev + 1]]
+            kp = int(np.searchsorted(row, prev))
+            common = np.nonzero(np.isin(row, prow, assume_unique=True) & (row != prev))[0]
+            c = len(common)
+            mode = mode_of(c, d)
+            ndir = (d + 511) // 512 if d > 512 else 0
+            F = 160 if 0 < ndir <= 8 else 288
+            fset = set()
+            if mode == "region":
+                for k in common:
+                    ulo = ((int(k) << 32) + d - 1) // d
+                    uhi = (((int(k) + 1) << 32) + d - 1) // d - 1
+                    for b in range(bounded(ulo, F), bounded(uhi, F) + 1):
+                        fset.add(b)
+            cset = set(common.tolist())
+            steps += 1
+            add(f"mode_{mode}")
+            trial = 0
+            while True:
+                u = philox(c0, c1, t, trial, k0, k1)
+                trial += 1
+                if trial == 1:
+                    Z = (ap_ + c) + (d - 1 - c) * aq
+                    r = u[0] * 2.3283064365386963e-10 * Z
+                    if r < ap_:
+                        add("branch_return")
+                        break
+                    if r - ap_ < c:
+                        add("branch_common")
+                        if mode == "region":
+                            add("sectors_region_select_block")
+                            if ndir > 8:
+                                add("sectors_region_directory")
+                        break
+                    add("branch_other")
+                k = bounded(u[1], d)
+                if mode == "region" and k != kp and bounded(u[1], F) in fset:
+                    add("sectors_region_membership_word")
+                if k != kp and k not in cset:
+                    break
+                add("other_retries")
+    res = {"graph": f"R-MAT-{a.scale}", "p": a.p, "q": a.q, "walks": a.walks, "steps_modelled": steps}
+    for k, v in sorted(cnt.items()):
+        res[k + "_per_step"] = v / steps
+    extra = sum(v for k, v in cnt.items() if k.startswith("sectors_")) / steps
+    res["extra_region_sectors_per_step"] = extra
+    res["model_read_sectors_per_step"] = 1.0 + extra + 2.0 / L  # + entry; + walk starts (order, offsets)
+    try:
+        pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))
+        e = pmc[f"n2v_rmat{a.scale}_p{a.p}_q{a.q}_L80_r10_bitset"]
+        res["measured_fabric_read_requests_per_step"] = e["fabric_read_requests_per_launch"] / e["walk_steps_per_launch"]
+    except Exception:
+        pass
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
