@@ -40,14 +40,14 @@ def bounded(x, d):
     return (x * d) >> 32
 
 
-def mode_of(c, d):
-    if c <= 20 and d < 65536:
+def mode_of(c, d, list_max=20, bits=320):
+    if c <= list_max and d < 65536:
         return "list"
-    if d <= 320:
+    if d <= bits:
         return "inline"
     if c > 0:
         l = int(np.floor(np.log2(d // c))) if d // c > 0 else 0
-        if c * l + c + ((d - 1) >> l) + 1 <= 320:
+        if c * l + c + ((d - 1) >> l) + 1 <= bits:
             return "ef"
     return "region"
 
@@ -59,6 +59,13 @@ def main():
     ap.add_argument("--q", type=float, default=4.0)
     ap.add_argument("--walks", type=int, default=600)
     ap.add_argument("--seed", type=int, default=42)
+    # what-if knobs (defaults = the built kernel): payload bits, list length,
+    # filter buckets with / without an in-entry directory, in-entry directory limit
+    ap.add_argument("--payload-bits", type=int, default=320)
+    ap.add_argument("--list-max", type=int, default=20)
+    ap.add_argument("--filter-dir", type=int, default=160)
+    ap.add_argument("--filter-nodir", type=int, default=288)
+    ap.add_argument("--pdir", type=int, default=8, help="directory blocks kept in the entry (0: none)")
     a = ap.parse_args()
     import gwamd
     import oracle
@@ -88,9 +95,9 @@ def main():
             kp = int(np.searchsorted(row, prev))
             common = np.nonzero(np.isin(row, prow, assume_unique=True) & (row != prev))[0]
             c = len(common)
-            mode = mode_of(c, d)
+            mode = mode_of(c, d, a.list_max, a.payload_bits)
             ndir = (d + 511) // 512 if d > 512 else 0
-            F = 160 if 0 < ndir <= 8 else 288
+            F = a.filter_dir if 0 < ndir <= a.pdir else a.filter_nodir
             fset = set()
             if mode == "region":
                 for k in common:
@@ -115,7 +122,7 @@ def main():
                         add("branch_common")
                         if mode == "region":
                             add("sectors_region_select_block")
-                            if ndir > 8:
+                            if ndir > a.pdir:
                                 add("sectors_region_directory")
                         break
                     add("branch_other")
