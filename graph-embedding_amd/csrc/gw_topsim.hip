@@ -132,7 +132,8 @@ __device__ __forceinline__ int upper_bound_i32(const int32_t* a, int n, int x) {
 // 256 bins from the top (desc) or from the bottom (asc); 4 bins per lane and
 // one wave scan instead of a serial 256-step loop.  Returns (bin, keys in
 // the bins scanned before it) through *bin / *before (lane 0 writes them).
-__device__ __forceinline__ void select_bin(const unsigned* hist, int need, bool desc, int* bin, int* before) {
+__device__ __forceinline__ void select_bin(const unsigned* hist, int need, bool desc, int* bin, int* before,
+                                           int* total = nullptr) {
   const int lane = threadIdx.x & 63;
   int c[4], loc = 0;
 #pragma unroll
@@ -160,9 +161,11 @@ __device__ __forceinline__ void select_bin(const unsigned* hist, int need, bool 
   const int src = m ? __ffsll(m) - 1 : 63;
   const int o = __shfl(first >= 0 ? first : 255, src, 64);
   const int cb = __shfl(first >= 0 ? cum_at : run - c[3], src, 64);
+  const int tot = __shfl(inc, 63, 64);
   if (lane == 0) {
     *bin = desc ? 255 - o : o;
     *before = cb;
+    if (total) *total = tot;
   }
 }
 
@@ -193,7 +196,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   __shared__ int s_wave[TS_WAVES + 1];
   __shared__ long long s_red[TS_WAVES];
   __shared__ int s_size[L + 2];
-  __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount, s_bin, s_cum, s_exact;
+  __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount, s_bin, s_cum, s_exact, s_total;
   __shared__ unsigned long long s_prefix, s_mask;
   // the output phase's selection arrays share LDS with the levels' child
   // offsets / the walkers' spawner offsets (binary-searched per child / walker)
@@ -631,25 +634,23 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     }
     if (A.out_ids) {
       const int K = A.topk;
-      long long c_local = 0;
-      for (int idx = tid; idx < NC; idx += TS_BLOCK) {
-        int32_t id;
-        double v;
-        if (cand(idx, &id, &v)) ++c_local;
-      }
-      const int C = (int)block_sum<long long>(c_local, s_red);
+      // the K-th key's bin may be taken whole once everything at or above it
+      // fits the selection arrays: the ordering pass below then ranks the
+      // extra entries out (bounded so that it keeps 4 threads per entry)
+      const int kcoll = max(K, TS_BLOCK / 4);
       mark(5);
       unsigned long long T = 0;  // threshold key (K-th largest)
       int32_t idT = 0x7fffffff;  // largest id taken at key == T
-      bool take_all = (C <= K);
+      bool take_all = false;     // at most K candidates (counted by the first radix pass)
       bool bin_exact = false;    // the K-th key's bin is taken whole: select by masked prefix
       unsigned long long Tmask = ~0ull;
-      if (!take_all) {
+      {
         if (tid == 0) {
           s_prefix = 0;
           s_mask = 0;
           s_need = K;
           s_exact = 0;
+          s_total = 0;
         }
         __syncthreads();
         for (int shift = 56; shift >= 0; shift -= 8) {
@@ -664,12 +665,16 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
             if ((k & msk) == pre) atomicAdd(&s_hist[(k >> shift) & 255], 1u);
           }
           __syncthreads();
-          if (tid < 64) select_bin(s_hist, s_need, true, &s_bin, &s_cum);
+          if (tid < 64) select_bin(s_hist, s_need, true, &s_bin, &s_cum, shift == 56 ? &s_total : nullptr);
           __syncthreads();
+          if (shift == 56 && s_total <= K) {
+            take_all = true;
+            break;
+          }
           if (tid == 0) {
             const int rest = s_need - s_cum;
-            // the chosen bin holds exactly the keys still needed: all of it is taken
-            if ((int)s_hist[s_bin] == rest) s_exact = 1;
+            // everything above the chosen bin (K - rest keys) plus the bin fits
+            if (K - rest + (int)s_hist[s_bin] <= kcoll) s_exact = 1;
             s_need = rest;
             s_prefix = pre | ((unsigned long long)s_bin << shift);
             s_mask = msk | (255ull << shift);

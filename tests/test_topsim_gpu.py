@@ -86,7 +86,7 @@ def test_topsim_variants(gw, oracle, variant, sample, step):
     assert st[1] == rst["pair_updates"]
 
 
-@pytest.mark.parametrize("name,k", [("moreno", 20), ("blog", 20), ("arxiv", 100)])
+@pytest.mark.parametrize("name,k", [("moreno", 20), ("blog", 20), ("arxiv", 100), ("arxiv", 3), ("blog", 200), ("blog", 256)])
 def test_topk_selection(gw, oracle, name, k):
     import torch
     from gwamd import _lib as Cl
