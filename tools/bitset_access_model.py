@@ -87,6 +87,7 @@ def main():
     for i in range(a.walks):
         w = begin + i
         c0, c1 = w & M32, (w >> 32) & M32
+        last_ret = False
         for t in range(2, int(lens[i])):
             prev, cur = int(W[i, t - 2]), int(W[i, t - 1])
             row = nbrs[off[cur]:off[cur + 1]]
@@ -117,7 +118,11 @@ def main():
                     r = u[0] * 2.3283064365386963e-10 * Z
                     if r < ap_:
                         add("branch_return")
+                        if last_ret:
+                            add("return_after_return")  # entry = the one read two steps earlier
+                        last_ret = True
                         break
+                    last_ret = False
                     if r - ap_ < c:
                         add("branch_common")
                         if mode == "region":

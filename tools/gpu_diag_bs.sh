@@ -4,6 +4,6 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 for dg in ${DIAGS:-0 1 2 3}; do
-  GW_DIAG_BS=$dg timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-topsim > gpurun_out/diag_$dg.json 2> gpurun_out/diag_$dg.err || { echo FAIL $dg; tail -5 gpurun_out/diag_$dg.err; exit 1; }
+  GW_DIAG_BS=$dg timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --secondary none > gpurun_out/diag_$dg.json 2> gpurun_out/diag_$dg.err || { echo FAIL $dg; tail -5 gpurun_out/diag_$dg.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/diag_$dg.json'));print($dg, d['value'], d['roofline']['kernel_ms'])"
 done
