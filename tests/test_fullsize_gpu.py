@@ -5,6 +5,10 @@ size-independent properties plus oracle parity on windows of the same run:
   the Graph500 R-MAT scale-20 graph, GW_N2V_BITSET — every step follows an
   edge, every iteration starts every vertex once, shard invariance, counters,
   and bit-exact oracle parity on walk windows;
+* config 4: R-MAT-24 ef 16, p=1 q=0.5, GW_N2V_REJECTION (slot entries + per-row
+  neighbour hash sets) and the north-star 10M/100M graph (R-MAT-24 ef 6,
+  p=0.25 q=4, GW_N2V_BITSET, 53.6 GB of tables): one walk per vertex — starts a
+  permutation, lengths, sampled steps follow edges, bit-exact oracle windows;
 * config 5: TopSim_singleSample on the 10M-vertex Java-semantics R-MAT graph
   (STEP 3, SAMPLE 1000, top-100) — oracle parity for sampled sources and the
   top-k invariants for a block of sources."""
@@ -104,3 +108,46 @@ def test_p10m_topsim_sources(gw, oracle):
     for r, s in enumerate(pick):
         k = int((I[r] >= 0).sum())
         assert np.all(np.diff(S[r, :k]) <= 0) and s not in I[r, :k] and np.all(S[r, :k] > 0)
+
+
+def _one_walk_per_vertex(gw, oracle, G, p, q, mode, seed, oracle_fn):
+    import torch
+    from gwamd import _lib as C
+    C.check(C.lib().gw_n2v_prepare(G.handle, p, q, mode), G.handle)
+    n, L = G.n, 80
+    out = torch.empty((n, L), dtype=torch.int32, device="cuda")
+    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    C.check(C.lib().gw_n2v_walks(G.handle, L, seed, 0, n, 1, C.ptr(out), C.ptr(lens), C.ptr(cnt), None), G.handle)
+    torch.cuda.synchronize()
+    csr = G.export_csr()
+    offs, nbrs = csr["offsets"], csr["nbrs"]
+    deg = np.diff(offs)
+    starts = out[:, 0].cpu().numpy()
+    np.testing.assert_array_equal(np.sort(starts), np.arange(n))  # iteration 0 starts every vertex once
+    ln = lens.cpu().numpy()
+    np.testing.assert_array_equal(ln, np.where(deg[starts] > 0, L, 1))
+    assert int(cnt[0].item()) == int((ln - 1).sum())
+    rows = np.random.default_rng(0).integers(0, n, 2000)
+    W = out[torch.as_tensor(rows, device="cuda")].cpu().numpy()
+    W = W[ln[rows] == L]
+    assert _is_edge(offs, nbrs, W[:, :-1].ravel(), W[:, 1:].ravel()).all()
+    for begin in (0, n // 2 + 777, n - 1000):
+        ref, rl, _ = oracle_fn(csr, p, q, seed, L, begin, 1000, nthreads=8)
+        np.testing.assert_array_equal(out[begin:begin + 1000].cpu().numpy(), ref)
+        np.testing.assert_array_equal(ln[begin:begin + 1000], rl)
+    return int(cnt[1].item()) / max(int(cnt[0].item()), 1)
+
+
+def test_config4_rejection_rmat24(gw, oracle):
+    from gwamd import _lib as C
+    G = gw.GWGraph.rmat(24, 16, 0.57, 0.19, 0.19, 42).to_device(0)
+    fn = lambda c, *a, **k: oracle.walks_scale(dict(c, weights=None), *a, **k)  # noqa: E731
+    trials = _one_walk_per_vertex(gw, oracle, G, 1.0, 0.5, C.N2V_REJECTION, 42, fn)
+    assert 1.0 <= trials < 1.1  # lazy rejection: ~1.03 trials per step at p=1 q=0.5
+
+
+def test_northstar_bitset_rmat24_ef6(gw, oracle):
+    from gwamd import _lib as C
+    G = gw.GWGraph.rmat(24, 6, 0.57, 0.19, 0.19, 43).to_device(0)
+    _one_walk_per_vertex(gw, oracle, G, 0.25, 4.0, C.N2V_BITSET, 42, oracle.walks_bitset)
