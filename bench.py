@@ -562,7 +562,7 @@ def main():
                                    f"(ef {args.edge_factor}, a,b,c=0.57,0.19,0.19, seed {args.seed}; n={n}, "
                                    f"adjacency entries={nnz}), walk_length={L}, {args.num_walks} walks/node per "
                                    f"rank per step",
-                       "global_batch": B * world, "seq_len": L, "parallelism": f"dp{world}",
+                       "walks_per_step": B * world, "walk_length": L, "parallelism": f"replicated graph, walks sharded over {world} rank(s)",
                        "allgather": bool(gather is not None)},
             "walk_steps": steps_total,
             "sampler": mode, "prepare_seconds": prep_s, "sampler_tables_gb": sampler_gb,
