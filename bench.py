@@ -1,39 +1,57 @@
 #!/usr/bin/env python3
 """bench.py — node2vec walk-steps/s on MI355X (+ TopSim pair-updates/s).
 
-Headline (BASELINE.json configs[1]): node2vec p=0.25 q=4 on a synthetic
-Graph500 R-MAT scale-20 graph (a,b,c = 0.57,0.19,0.19, edge factor 16, seed
-42, symmetrised, deduplicated, no self loops), walk_length 80, 10 walks per
-node.  One "step" = one pass of the hot path over one batch: 10 walks from
-every vertex (6.47M walks, ~5.1e8 walk-steps) written to HBM.
+Headline (BASELINE.json configs[1], `--config 2`, the default): node2vec
+p=0.25 q=4 on a synthetic Graph500 R-MAT scale-20 graph (a,b,c = 0.57,0.19,
+0.19, edge factor 16, seed 42, symmetrised, deduplicated, no self loops),
+walk_length 80, 10 walks per node.  One "step" = one pass of the hot path over
+one batch: 10 walks from every vertex (6.47M walks, ~5.1e8 walk-steps) written
+to HBM, per rank.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config {2,4,5}]
 
-N>1: launched by torch.distributed.run, one rank per GPU.  The graph is
-replicated; each rank walks its own block of global walk indices (walks are
-a pure function of (seed, global walk index), so shards never overlap and
-need no collective).  `value` = walk-steps of all ranks / max-over-ranks
-time ("scaling": "weak").  `--allgather` adds the RCCL all-gather of the
-emitted walks (north_star option) inside the timed step.
+Ranks.  `--gpus N > 1` without WORLD_SIZE in the environment: bench.py starts
+`python -m torch.distributed.run --nproc-per-node N` as a CHILD process (before
+anything touches the GPU) and exits with its status; with WORLD_SIZE set (the
+driver's own torch.distributed.run launch) it must equal N.  One rank per GPU,
+backend "nccl" (= RCCL over xGMI); GW_DIST_BACKEND=gloo overrides it (CPU
+rehearsals).  The graph is replicated; rank r walks the global walk-index block
+(step*world + r)*B: walks are a pure function of (seed, global walk index), so
+shards never overlap and need no collective ("scaling": "weak").  `value` =
+walk-steps of all ranks / max-over-ranks time.  At world > 1 the RCCL
+all-gather of the emitted walks (north_star) is timed as a second measurement
+(`allgather` in the same JSON line: walk + all-gather per step), and rank 0
+checks the gathered block of the last rank byte-for-byte against its own
+recomputation of that block.
 
-Also reported (same JSON line):
-  roofline      36 algorithmic bytes per walk-step / kernel time,
-                kernel time from HIP events on the launch stream; traffic from
-                the committed rocprofv3 PMC pass (profiles/), or null.
-  cpu_baseline  the oracle's C restatement of the same sampling (OpenMP),
-                timed on a bounded sample of the same workload (rank 0, N=1).
-  secondary     .topsim: TopSim_singleSample on lshrank blog (STEP=5,
-                SAMPLE=10000, C=0.6, top-20, all 10,313 sources): pair-updates/s
-                (--topsim-graphs adds arxiv / moreno / p10m under .topsim.more);
-                .walk_10m / .walk_10m_p1q1: the north_star's 10M-node/100M-edge
-                graph (R-MAT scale 24, ef 6), 1 walk per node, at the bench's
-                p/q and at p=q=1, each with its CPU sample;
-                .simrank_naive: SimRank.java (STEP=3, C=0.6) on blog, dense
-                10,313^2 fp64 result: rounds/s, LDS-gather roofline.
+Configs (BASELINE.json):
+  2  headline above; secondaries (1 GPU): TopSim on lshrank blog (config 3),
+     the north_star 10M/100M graph at the bench's p/q and at p=q=1, config 4 and
+     config 5 on one GPU, naive SimRank on blog.  At world > 1 the secondaries
+     are configs 4 and 5, sharded.
+  4  node2vec p=1 q=0.5 on R-MAT-24 ef 16 (rejection sampler), 1 walk/node per
+     rank per step as the headline.
+  5  TopSim_singleSample on the 10M-vertex power-law graph (top-100, STEP 3,
+     SAMPLE 1000): all non-isolated sources split over the ranks (strong
+     scaling); value = pair-updates/s.
+
+Also in the JSON line:
+  roofline      36 algorithmic bytes per walk-step / kernel time
+                (HIP events on the launch stream); traffic = HBM bytes per launch
+                from the committed rocprofv3 PMC summary of this exact library
+                build (profiles/pmc_summary.json), or null; random_line_roofline
+                = fabric read requests/s vs the calibrated random-block rate for
+                the sampler tables' size (profiles/calib_r02.json).
+  cpu_baseline  the oracle's C restatement of the same sampling (OpenMP), timed
+                on a bounded sample of the same workload (rank 0, N=1).
+`--plumbing-check` runs the launcher, rank and collective path with synthetic
+rows and no GPU work (CPU gloo test of this file); it reports no throughput.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -45,23 +63,32 @@ BYTES_PER_STEP = 36       # row bounds 16 + alias q/J 12 + nbr 4 + 
 TOPSIM_B_EXT = 52         # per path-extension
 TOPSIM_B_UPD = 24         # per pair-update
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
-RANDOM_LINE_PEAK = 4.9e10 # measured: random 64 B sectors, one load instruction each, 8-32 GB tables (tools/calib/calib_sweep.hip)
+L2_PEAK_GBS = 34500.0     # MI355X_MICROARCH.md §L2: 32 MiB aggregate, ~34.5 TB/s
+CALIB_FILE = os.path.join(ROOT, "profiles", "calib_r02.json")
+GATHER_FULL_LIMIT = int(os.environ.get("GW_BENCH_GATHER_LIMIT", 48 << 30))  # gathered walks kept whole per rank; above: chunked ring
 
 
-def parse():
+def parse(argv):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: WORLD_SIZE, else 1")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--scale", type=int, default=20)
+    ap.add_argument("--config", type=int, choices=[2, 4, 5], default=2,
+                    help="BASELINE.json config timed as the headline")
+    ap.add_argument("--scale", type=int, default=None)
     ap.add_argument("--edge-factor", type=int, default=16)
-    ap.add_argument("--p", type=float, default=0.25)
-    ap.add_argument("--q", type=float, default=4.0)
+    ap.add_argument("--rmat-params", choices=["graph500", "reference"], default="graph500",
+                    help="R-MAT (a,b,c): Graph500 0.57/0.19/0.19 (SURVEY §8d) or the reference "
+                         "generator's 0.45/0.15/0.15 (RMATGraphGenerator.java:179-182)")
+    ap.add_argument("--p", type=float, default=None)
+    ap.add_argument("--q", type=float, default=None)
     ap.add_argument("--walk-length", type=int, default=80)
-    ap.add_argument("--num-walks", type=int, default=10)
+    ap.add_argument("--num-walks", type=int, default=None, help="walks per node per rank per step")
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--allgather", action="store_true")
-    ap.add_argument("--mode", choices=["auto", "bitset", "rejection"], default="auto",
+    ap.add_argument("--allgather", choices=["auto", "on", "off"], default="auto",
+                    help="time the RCCL all-gather of the walks (auto: when ranks > 1)")
+    ap.add_argument("--mode", choices=["auto", "bitset", "rejection"], default=None,
                     help="second-order sampler (auto: bitset when it fits in HBM)")
     ap.add_argument("--no-topsim", action="store_true")
     ap.add_argument("--no-simrank", action="store_true")
@@ -71,76 +98,69 @@ def parse():
     ap.add_argument("--walk10m-edge-factor", type=int, default=6)
     ap.add_argument("--simrank-graph", default="blog", help="naive SimRank graph (blog or moreno)")
     ap.add_argument("--simrank-rounds", type=int, default=3, help="SimRank.java STEP")
-    ap.add_argument("--no-rmat24", action="store_true",
-                    help="skip config 4 (R-MAT-24 ef 16, p=1 q=0.5) on this GPU")
+    ap.add_argument("--no-rmat24", action="store_true", help="skip config 4 as a secondary")
+    ap.add_argument("--no-p10m", action="store_true", help="skip config 5 as a secondary")
+    ap.add_argument("--no-arxiv", action="store_true",
+                    help="skip the arxiv line (same graph as the reference CPU fixture)")
     ap.add_argument("--secondary", choices=["auto", "all", "none"], default="auto",
-                    help="secondary workloads: auto = all at 1 GPU, none when ranks > 1 (scaling runs time "
-                         "the headline only)")
+                    help="secondary workloads: auto = all at 1 GPU, configs 4 and 5 (sharded) at ranks > 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--topsim-sample", type=int, default=10000)
     ap.add_argument("--topsim-step", type=int, default=5)
-    ap.add_argument("--topsim-graphs", default="blog", help="comma list of blog,arxiv,moreno,p10m")
-    return ap.parse_args()
+    ap.add_argument("--topsim-graphs", default="blog", help="comma list of blog,arxiv,moreno")
+    ap.add_argument("--plumbing-check", action="store_true",
+                    help="ranks + collectives with synthetic rows, no GPU work, no throughput")
+    a = ap.parse_args(argv)
+    cfg = {2: dict(scale=20, p=0.25, q=4.0, num_walks=10, mode="auto"),
+           4: dict(scale=24, p=1.0, q=0.5, num_walks=1, mode="rejection"),
+           5: dict(scale=20, p=0.25, q=4.0, num_walks=10, mode="auto")}[a.config]
+    for k, v in cfg.items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    return a
+
+
+def rmat_abc(args):
+    return (0.57, 0.19, 0.19) if args.rmat_params == "graph500" else (0.45, 0.15, 0.15)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(csr, args, sample_walk0):
-    """Oracle (C restatement, OpenMP) on a bounded sample of the same walks."""
-    import oracle
-    import numpy as np
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except Exception:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
-    c = dict(offsets=csr["offsets"], nbrs=csr["nbrs"], weights=None, node_order=csr["node_order"])
-    L = args.walk_length
-    nw = 20000
-    t0 = time.perf_counter()
-    _, lens, _ = oracle.walks_scale(c, args.p, args.q, args.seed, L, sample_walk0, nw, nthreads=cores)
-    dt = time.perf_counter() - t0
-    nw2 = int(min(3_000_000, max(nw, nw * args.cpu_seconds / max(dt, 1e-3))))
-    t0 = time.perf_counter()
-    _, lens, _ = oracle.walks_scale(c, args.p, args.q, args.seed, L, sample_walk0, nw2, nthreads=cores)
-    dt = time.perf_counter() - t0
-    steps = int((lens.astype(np.int64) - 1).sum())
-    return {"value": steps / dt, "unit": "walk-steps/s", "cores": cores, "kind": "port",
-            "sample": f"{nw2} walks ({steps} walk-steps) of the same R-MAT-{args.scale} p={args.p} q={args.q} "
-                      f"L={L} workload, oracle/oracle.c or_walks_scale, {dt:.1f} s",
-            "reference_python_context": "reference node2vec.py measured 41,266 walk-steps/s/core on "
-                                        "RMAT-12 in the build container (SURVEY §6); it cannot run at scale 20 "
-                                        "(per-edge alias tables need 7.0e10 entries)"}
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
-def topsim_cpu_baseline(tg, sample, step, args):
-    """Oracle restatement of TopSim_singleSample (Java-literal queue, OpenMP
-    over sources) on a bounded prefix of the same sources."""
-    import oracle
-    import numpy as np
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except Exception:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
-    n = tg.getVCount()
-    ns = min(n, 256)
-    t0 = time.perf_counter()
-    _, st = oracle.topsim(tg._offs, tg._nbrs, 0, sample, step, C=0.6, seed=args.seed,
-                          sources=np.arange(ns, dtype=np.int32), nthreads=cores)
-    dt = time.perf_counter() - t0
-    ns2 = int(min(n, max(ns, ns * args.cpu_seconds / max(dt, 1e-3))))
-    t0 = time.perf_counter()
-    _, st = oracle.topsim(tg._offs, tg._nbrs, 0, sample, step, C=0.6, seed=args.seed,
-                          sources=np.arange(ns2, dtype=np.int32), nthreads=cores)
-    dt = time.perf_counter() - t0
-    return {"value": st["pair_updates"] / dt, "unit": "pair-updates/s", "cores": cores, "kind": "port",
-            "sample": f"sources 0..{ns2 - 1} ({st['pair_updates']} pair-updates), oracle/oracle.c or_topsim "
-                      f"(TopSim_singleSample.java queue restated), {dt:.1f} s; the Java reference cannot run "
-                      "here (no JDK)"}
+def launch_ranks(args, argv):
+    """--gpus N > 1 outside torch.distributed.run: run it as a child (no exec,
+    nothing has touched the GPU in this process) and return its exit status;
+    rank 0's JSON line reaches our stdout through the inherited descriptor."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    log(f"[bench] launching {args.gpus} ranks: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd, env=env)
+
+
+# ---- calibrations / committed profiles ---------------------------------------
+def calib_rate(table_bytes, block=64):
+    """Random-block read rate (blocks/s) measured by tools/calib/calib_sweep.hip
+    (profiles/calib_r02.json: dependent reads, 5 waves/SIMD) for the table size
+    nearest (log scale) to `table_bytes`."""
+    import math
+    with open(CALIB_FILE) as f:
+        d = json.load(f)["dep_w5_blocks_per_s"][str(block)]
+    mb = max(1.0, table_bytes / 2**20)
+    key = min(d, key=lambda k: abs(math.log(float(k)) - math.log(mb)))
+    return float(d[key]), int(key)
 
 
 def lib_digest():
@@ -150,62 +170,258 @@ def lib_digest():
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
-def load_traffic(tag, launch_steps):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, only
-    when it was measured on this exact library build and workload."""
+def load_prof(tag, units=None, key="walk_steps_per_launch"):
+    """PMC summary entry measured on this exact library build (and workload)."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(p) as f:
-            d = json.load(f)
-        e = d.get(tag)
-        if e and e.get("walk_steps_per_launch") == launch_steps and e.get("lib_sha256") == lib_digest():
+            e = json.load(f).get(tag)
+        if e and e.get("lib_sha256") == lib_digest() and (units is None or e.get(key) == units):
             return e
     except Exception:
         pass
     return None
 
 
-def main():
-    args = parse()
-    import numpy as np
-    import torch
-    import torch.distributed as dist
+def cores_used():
+    try:
+        c = len(os.sched_getaffinity(0))
+    except Exception:
+        c = os.cpu_count() or 1
+    return max(1, min(c, 16))
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    if args.secondary == "none" or (args.secondary == "auto" and world > 1):
-        args.no_topsim = args.no_walk10m = args.no_simrank = args.no_rmat24 = True
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        local = local % max(1, torch.cuda.device_count())  # (ranks > GPUs only in rehearsals)
-        torch.cuda.set_device(local)
-        backend = os.environ.get("GW_DIST_BACKEND", "nccl")  # nccl == RCCL on ROCm
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+# ---- CPU baselines (oracle: rank 0, N=1 only) --------------------------------
+def cpu_baseline_walks(csr, p, q, seed, L, walk0, seconds, max_walks=3_000_000):
+    """Oracle (C restatement of the rejection sampler, OpenMP) on a bounded sample."""
+    import numpy as np
+    import oracle
+    cores = cores_used()
+    c = dict(offsets=csr["offsets"], nbrs=csr["nbrs"], weights=None, node_order=csr["node_order"])
+    nw = 2000
+    t0 = time.perf_counter()
+    oracle.walks_scale(c, p, q, seed, L, walk0, nw, nthreads=cores)
+    dt = time.perf_counter() - t0
+    nw = int(min(max_walks, max(nw, nw * seconds / max(dt, 1e-3))))
+    t0 = time.perf_counter()
+    _, lens, _ = oracle.walks_scale(c, p, q, seed, L, walk0, nw, nthreads=cores)
+    dt = time.perf_counter() - t0
+    steps = int((lens.astype(np.int64) - 1).sum())
+    return {"value": steps / dt, "unit": "walk-steps/s", "cores": cores, "kind": "port",
+            "sample": f"{nw} walks ({steps} walk-steps) of the same graph, p={p} q={q} L={L}, "
+                      f"oracle/oracle.c or_walks_scale (rejection sampler, same walk law), {dt:.1f} s"}
+
+
+def cpu_baseline_topsim(offs, nbrs, n, sample, step, seed, seconds, sources=None):
+    """Oracle restatement of TopSim_singleSample (Java-literal queue, OpenMP
+    over sources) on a bounded prefix of the same sources."""
+    import numpy as np
+    import oracle
+    cores = cores_used()
+    srcs = np.arange(n, dtype=np.int32) if sources is None else np.asarray(sources, np.int32)
+    ns = min(len(srcs), 256)
+    t0 = time.perf_counter()
+    oracle.topsim(offs, nbrs, 0, sample, step, C=0.6, seed=seed, sources=srcs[:ns], nthreads=cores)
+    dt = time.perf_counter() - t0
+    ns2 = int(min(len(srcs), max(ns, ns * seconds / max(dt, 1e-3))))
+    t0 = time.perf_counter()
+    _, st = oracle.topsim(offs, nbrs, 0, sample, step, C=0.6, seed=seed, sources=srcs[:ns2], nthreads=cores)
+    dt = time.perf_counter() - t0
+    return {"value": st["pair_updates"] / dt, "unit": "pair-updates/s", "cores": cores, "kind": "port",
+            "sample": f"the first {ns2} sources ({st['pair_updates']} pair-updates), oracle/oracle.c or_topsim "
+                      f"(TopSim_singleSample.java queue restated), {dt:.1f} s; the Java reference cannot run "
+                      "here (no JDK)"}
+
+
+def reference_cpu_fixture():
+    """profiles/cpu_reference_node2vec.json: the reference node2vec.py walk
+    loop timed in the build container (tools/ref_cpu_node2vec.py)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "cpu_reference_node2vec.json")) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
+# ---- ranks and collectives -----------------------------------------------------
+class Ranks:
+    def __init__(self, args):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.backend = None
+        self.plumbing = args.plumbing_check
+        import torch
+        self.torch = torch
+        if self.world > 1:
+            import torch.distributed as dist
+            self.dist = dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            self.backend = "gloo" if self.plumbing else os.environ.get("GW_DIST_BACKEND", "nccl")
+        if self.plumbing:
+            self.dev = torch.device("cpu")
+            self.ngpu = 0
         else:
-            dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+            ndev = torch.cuda.device_count()
+            if ndev < 1:
+                raise SystemExit("bench.py: no GPU visible (use --plumbing-check for the CPU rehearsal)")
+            self.ngpu = min(self.world, ndev)
+            torch.cuda.set_device(self.local % ndev)  # ranks > GPUs only in gloo rehearsals
+            self.dev = torch.device("cuda", torch.cuda.current_device())
+        if self.world > 1:
+            if self.backend == "nccl":
+                self.dist.init_process_group("nccl", device_id=self.dev)  # RCCL
+            else:
+                self.dist.init_process_group(self.backend)
+            got = self.dist.get_world_size()
+            if got != self.world:
+                raise SystemExit(f"bench.py: process group has {got} ranks, WORLD_SIZE={self.world}")
+        self.cdev = self.dev if self.backend == "nccl" else torch.device("cpu")
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def sync(self):
+        if self.dev.type == "cuda":
+            self.torch.cuda.synchronize()
+
+    def allreduce(self, vals, op="sum", dtype=None):
+        """Reduce a list of numbers over ranks (op: sum | max)."""
+        if self.world == 1:
+            return list(vals)
+        torch = self.torch
+        t = torch.tensor(list(vals), dtype=dtype or torch.float64, device=self.cdev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
+        return t.tolist()
+
+    def allgather_into(self, out, src):
+        """out[world * rows] = every rank's src[rows] (rank order)."""
+        if self.backend == "gloo" and src.device.type == "cuda":
+            tmp = self.torch.empty(out.shape, dtype=out.dtype)
+            self.dist.all_gather_into_tensor(tmp, src.cpu())
+            out.copy_(tmp)
+        else:
+            self.dist.all_gather_into_tensor(out, src)
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def time_steps(R, step, steps, warmup, stream=None, events=True):
+    """Warm-up, then K steps bracketed by barrier + synchronize on both sides;
+    returns (max-over-ranks seconds, mean kernel ms from HIP events or None)."""
+    torch = R.torch
+    for i in range(warmup):
+        step(i, None)
+    R.sync()
+    evs = None
+    if events and R.dev.type == "cuda":
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    R.barrier()
+    R.sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(warmup + i, evs[i] if evs else None)
+    R.sync()
+    R.barrier()
+    el = time.perf_counter() - t0
+    el = R.allreduce([el], "max")[0]
+    kms = None
+    if evs:
+        kms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    return el, kms
+
+
+def gather_timing(R, args, step, out, L, B):
+    """walk + RCCL all-gather of the emitted walks per step (north_star's
+    exchange), timed like the headline; rank 0 then checks the last rank's
+    gathered block against its own recomputation of that block."""
+    torch = R.torch
+    row_bytes = L * 4
+    world = R.world
+    full = world * B * row_bytes <= GATHER_FULL_LIMIT
+    if full:
+        rows_c = B
+    else:  # chunked ring (SURVEY §8e): 256 MB per rank per call into a reused buffer
+        rows_c = max(1, min(B, (256 << 20) // row_bytes, GATHER_FULL_LIMIT // (world * row_bytes)))
+    gbuf = torch.empty((world * rows_c, L), dtype=torch.int32, device=R.dev)
+
+    def gstep(i, ev):
+        step(i, ev)
+        for r0 in range(0, B, rows_c):
+            n = min(B, r0 + rows_c) - r0
+            R.allgather_into(gbuf[:world * n], out[r0:r0 + n])  # rank-major [rank][n rows]
+    el, _ = time_steps(R, gstep, args.steps, 0, events=False)
+    # check: the last timed step's gathered block of rank world-1 (full mode) or
+    # the last chunk (ring mode) equals what this rank computes for that block
+    check = None
+    last = args.steps - 1
+    rl = world - 1
+    if R.rank == 0:
+        from gwamd import dist as gdist
+        w_last = gdist.weak_block(last, world, rl, B)
+        if full:
+            got = gbuf[rl * B:(rl + 1) * B].clone()
+            lo, n = 0, B
+        else:
+            lo = ((B - 1) // rows_c) * rows_c
+            n = B - lo
+            got = gbuf[rl * n:(rl + 1) * n].clone()
+        mine = step.recompute(w_last + lo, n)
+        check = bool(torch.equal(got.cpu(), mine.cpu()))
+    ok = R.allreduce([1.0 if (check is None or check) else 0.0], "max")
+    return {"seconds": el, "ms_per_step": el / args.steps * 1e3,
+            "gathered_bytes_per_step_per_rank": (world - 1) * B * row_bytes,
+            "mode": "whole" if full else f"ring of {rows_c}-row chunks",
+            "check_last_rank_block_identical": check}, ok
+
+
+# ---- workloads -----------------------------------------------------------------
+def walk_headline(R, args):
+    """Headline node2vec measurement (configs 2 and 4)."""
+    import numpy as np
+    torch = R.torch
+    from gwamd import dist as gdist
+    L = args.walk_length
+    world, rank = R.world, R.rank
+
+    if R.plumbing:
+        n = 1 << args.scale
+        B = args.num_walks * n
+        out = torch.empty((B, L), dtype=torch.int32)
+
+        def synth(w0, cnt):  # NOT walks: row w = (w*L + t) mod 2^31, for the rank/collective plumbing only
+            w = torch.arange(w0, w0 + cnt, dtype=torch.int64).unsqueeze(1)
+            return ((w * L + torch.arange(L, dtype=torch.int64)) % (2**31 - 1)).to(torch.int32)
+        def step(i, ev):
+            out.copy_(synth(gdist.weak_block(i, world, rank, B), B))
+        step.recompute = synth
+        el, _ = time_steps(R, step, args.steps, args.warmup, events=False)
+        steps_total = int(R.allreduce([args.steps * B * (L - 1)], "sum", torch.int64)[0])
+        res = {"value": None, "walk_steps": steps_total, "seconds": el, "n": n, "nnz": None, "mode": "plumbing",
+               "B": B}
+        if world > 1 and args.allgather != "off":
+            g, ok = gather_timing(R, args, step, out, L, B)
+            res["allgather"] = g
+            res["allgather_all_ranks_ok"] = bool(ok[0] >= 1.0)
+        return res
 
     import gwamd
     from gwamd import _lib as C
-    from gwamd import dist as gdist
-    L = args.walk_length
-
-    # ---- graph (host build, replicated on every rank) ----
+    a, b, c = rmat_abc(args)
     t0 = time.perf_counter()
-    G = gwamd.GWGraph.rmat(args.scale, args.edge_factor, 0.57, 0.19, 0.19, args.seed)
+    G = gwamd.GWGraph.rmat(args.scale, args.edge_factor, a, b, c, args.seed)
     inf = G.info()
     n, nnz = inf.n, inf.nnz
-    log(f"[rank {rank}] rmat-{args.scale}: n={n} nnz={nnz} maxdeg={inf.max_degree} "
+    log(f"[rank {rank}] rmat-{args.scale} ef {args.edge_factor}: n={n} nnz={nnz} maxdeg={inf.max_degree} "
         f"built in {time.perf_counter() - t0:.1f}s")
-    G.to_device(dev.index)
-    # sampler: per-edge 64 B entries + common-neighbour regions when they fit
-    # in HBM (exact 3-way mixture, ~1.5 lines per step), else rejection sampling
+    G.to_device(R.dev.index)
     t0 = time.perf_counter()
     mode = "bitset" if args.mode in ("auto", "bitset") else "rejection"
+    if args.p == 1.0 and args.q == 1.0:
+        mode = "rejection"
     if mode == "bitset":
         try:
             C.check(C.lib().gw_n2v_prepare(G.handle, args.p, args.q, C.N2V_BITSET), G.handle)
@@ -218,368 +434,490 @@ def main():
         C.check(C.lib().gw_n2v_prepare(G.handle, args.p, args.q, C.N2V_REJECTION), G.handle)
     torch.cuda.synchronize()
     prep_s = time.perf_counter() - t0
-    sampler_gb = G.info().sampler_bytes / 1e9
-    log(f"[rank {rank}] prepare ({mode}) {prep_s:.2f}s, sampler tables {sampler_gb:.2f} GB")
+    sampler_bytes = G.info().sampler_bytes
+    if args.p == 1.0 and args.q == 1.0:
+        mode = "first-order"
+    log(f"[rank {rank}] prepare ({mode}) {prep_s:.2f}s, sampler tables {sampler_bytes / 1e9:.2f} GB")
 
-    B = args.num_walks * n                      # walks per rank per step
-    out = torch.empty((B, L), dtype=torch.int32, device=dev)
-    cnt = torch.zeros(2, dtype=torch.int64, device=dev)
-    gather = None
-    if args.allgather and world > 1:
-        gather = torch.empty((world * B, L), dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    B = args.num_walks * n  # walks per rank per step
+    out = torch.empty((B, L), dtype=torch.int32, device=R.dev)
+    cnt = torch.zeros(2, dtype=torch.int64, device=R.dev)
+    stream = torch.cuda.current_stream(R.dev)
     sh = C.ctypes.c_void_p(stream.cuda_stream)
 
-    def step(i, events=None):
-        # global walk index block of (rank, step i): iterations
-        # num_walks*(i*world+rank) ... +num_walks-1 of the reference loop
+    def launch(w0, count, dst, counters):
+        C.check(C.lib().gw_n2v_walks(G.handle, L, args.seed, w0, count, 1, C.ptr(dst), None,
+                                     C.ptr(counters) if counters is not None else None, sh), G.handle)
+
+    def step(i, ev):
+        # global walk-index block of (rank, step i): iterations num_walks*(i*world+rank) ...
         w0 = gdist.weak_block(i, world, rank, B)
-        if events is not None:
-            events[0].record(stream)
-        C.check(C.lib().gw_n2v_walks(G.handle, L, args.seed, w0, B, 1, C.ptr(out), None, C.ptr(cnt), sh),
-                G.handle)
-        if events is not None:
-            events[1].record(stream)
-        if gather is not None:
-            dist.all_gather_into_tensor(gather, out)
+        if ev is not None:
+            ev[0].record(stream)
+        launch(w0, B, out, cnt)
+        if ev is not None:
+            ev[1].record(stream)
+
+    def recompute(w0, count):
+        dst = torch.empty((count, L), dtype=torch.int32, device=R.dev)
+        launch(w0, count, dst, None)
+        torch.cuda.synchronize()
+        return dst
+    step.recompute = recompute
 
     for i in range(args.warmup):
-        step(i)
+        step(i, None)
     torch.cuda.synchronize()
     cnt.zero_()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i, evs[i])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    steps_local = int(cnt[0].item())
-    trials_local = int(cnt[1].item())
-    kms = [a.elapsed_time(b) for a, b in evs]
-    k_avg_ms = sum(kms) / len(kms)
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-        s = torch.tensor([steps_local, trials_local], dtype=torch.int64, device=dev)
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        steps_total, trials_total = int(s[0].item()), int(s[1].item())
-    else:
-        steps_total, trials_total = steps_local, trials_local
+    el, k_avg_ms = time_steps(R, step, args.steps, 0)
+    steps_local, trials_local = int(cnt[0].item()), int(cnt[1].item())
+    steps_total, trials_total = (int(x) for x in R.allreduce([steps_local, trials_local], "sum", torch.int64))
     value = steps_total / el
     launch_steps = steps_local // args.steps
     achieved = BYTES_PER_STEP * launch_steps / (k_avg_ms * 1e-3) / 1e9
-    tag = f"n2v_rmat{args.scale}_p{args.p}_q{args.q}_L{L}_r{args.num_walks}_{mode}"
-    prof = load_traffic(tag, launch_steps)
+    kname = "k_walk_bitset" if mode == "bitset" else "k_walk_scale"
+    tag = f"n2v_rmat{args.scale}_ef{args.edge_factor}_p{args.p}_q{args.q}_L{L}_r{args.num_walks}_{mode}"
+    prof = load_prof(tag, launch_steps)
     traffic = prof["hbm_bytes_per_launch"] if prof else None
-    # random-line roofline: the kernel's 64 B fabric read requests per second
-    # against the calibrated random-gather rate (tools/calib: 4.8e10 lines/s)
-    line_rate = None
+    peak_lines, table_mb = calib_rate(sampler_bytes if mode == "bitset" else max(sampler_bytes, 16 * nnz))
+    line_rate = {"calibrated_peak_lines_per_s": peak_lines, "calib_table_mb": table_mb,
+                 "calib_file": os.path.relpath(CALIB_FILE, ROOT)}
     if prof and prof.get("fabric_read_requests_per_launch"):
         lr = prof["fabric_read_requests_per_launch"] / (k_avg_ms * 1e-3)
-        line_rate = {"achieved_lines_per_s": lr, "calibrated_peak_lines_per_s": RANDOM_LINE_PEAK,
-                     "frac": lr / RANDOM_LINE_PEAK,
-                     "lines_per_step": prof["fabric_read_requests_per_launch"] / max(launch_steps, 1)}
+        line_rate.update({"achieved_lines_per_s": lr, "frac": lr / peak_lines,
+                          "lines_per_step": prof["fabric_read_requests_per_launch"] / max(launch_steps, 1)})
 
-    # ---- parity spot check (cheap): every step follows an edge ----
-    if rank == 0 and not (os.environ.get("GW_DIAG_BS") or os.environ.get("GW_DIAG_NO_STORE")):  # (diag knobs: wrong walks)
+    # ---- parity spot check (cheap): every step of a sample follows an edge ----
+    if rank == 0:
         csr = G.export_csr()
         smp = out[:2000].cpu().numpy()
         offs, nbrs = csr["offsets"], csr["nbrs"]
-        a, b = smp[:, :-1].ravel(), smp[:, 1:].ravel()
-        pos = np.array([np.searchsorted(nbrs[offs[x]:offs[x + 1]], y) for x, y in zip(a, b)])
-        ok = all(nbrs[offs[x] + p] == y for x, y, p in zip(a, b, pos))
+        ok = True
+        for row in smp:
+            ln = int((row >= 0).sum())
+            for x, y in zip(row[:ln - 1], row[1:ln]):
+                s = nbrs[offs[x]:offs[x + 1]]
+                k = np.searchsorted(s, y)
+                if k >= len(s) or s[k] != y:
+                    ok = False
         if not ok:
             log("PARITY SPOT CHECK FAILED: a step does not follow an edge")
             sys.exit(3)
 
-    # ---- TopSim secondary metric (config 3: lshrank graphs) ----
-    TOPSIM_GRAPHS = {"blog": ("blog.txt", 10313, ",", "lshrank blog, V=10313, 333,983 edges"),
-                     "arxiv": ("arxiv_author_pub.txt", 38741, "\t", "lshrank arxiv, V=38741, 58,595 edges"),
-                     "moreno": ("moreno_crime_crime.txt", 1380, "\t", "lshrank moreno, V=1380, 1,476 edges")}
+    res = {"value": value, "walk_steps": steps_total, "seconds": el, "n": n, "nnz": nnz, "mode": mode,
+           "B": B, "prep_s": prep_s, "sampler_gb": sampler_bytes / 1e9,
+           "trials_per_step": trials_total / max(steps_total, 1),
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                        "traffic_note": (prof or {}).get("note"),
+                        "kernel": kname, "kernel_ms": k_avg_ms,
+                        "bytes_per_unit": BYTES_PER_STEP, "units_per_launch": launch_steps,
+                        "lib_sha256": lib_digest(), "random_line_roofline": line_rate}}
+    if world > 1 and args.allgather != "off":
+        g, ok = gather_timing(R, args, step, out, L, B)
+        g["value"] = steps_total / g["seconds"]
+        g["unit"] = "walk-steps/s (walks all-gathered to every rank)"
+        g["xgmi_GBps_per_rank"] = g["gathered_bytes_per_step_per_rank"] * args.steps / g["seconds"] / 1e9
+        res["allgather"] = g
+        res["allgather_all_ranks_ok"] = bool(ok[0] >= 1.0)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_walks(G.export_csr(), args.p, args.q, args.seed, L, 0, args.cpu_seconds)
+    del out
+    G.free()
+    return res
 
-    def run_topsim(name):
-        from gwamd import topsim
-        K = 20
-        sample, step = args.topsim_sample, args.topsim_step
-        if name == "p10m":
-            # config 5: 10M-vertex Java-semantics R-MAT (reference quadrant
-            # recursion), 1e8 generated lines, all non-isolated sources, top-100
-            t0 = time.perf_counter()
-            pg = gwamd.GWGraph.rmat_java(10_000_000, 100_000_000, 0.57, 0.19, 0.19, args.seed)
-            deg = np.diff(pg.export_csr()["offsets"])
-            log(f"[rank {rank}] p10m built in {time.perf_counter() - t0:.1f}s")
-            pg.to_device(dev.index)
-            h = pg.handle
-            srcs = np.nonzero(deg > 0)[0].astype(np.int32)
-            V = len(srcs)
-            desc = f"10M vertices, 1e8 R-MAT lines, {V} non-isolated sources"
-            K, sample, step = 100, 1000, 3
-            src = torch.as_tensor(srcs, device=dev)
-        else:
-            fname, V, sep, desc = TOPSIM_GRAPHS[name]
-            tg = topsim.Graph(os.path.join(ROOT, "tests", "golden", "data", fname), V, separator=sep,
-                              device=dev.index)
-            tg._ensure_device()
-            h = tg._g.handle
-            src = torch.arange(V, dtype=torch.int32, device=dev)
-        ids = torch.empty((V, K), dtype=torch.int32, device=dev)
-        sc = torch.empty((V, K), dtype=torch.float64, device=dev)
-        st = torch.zeros(4, dtype=torch.int64, device=dev)
 
-        def ts_run(stats_ptr):
-            C.check(C.lib().gw_topsim(h, C.TOPSIM_SINGLE_SAMPLE, sample, step, 0.6,
-                                      args.seed, C.ptr(src), V, K, C.ptr(ids), C.ptr(sc), stats_ptr, sh), h)
+def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejection=False, walks_per_node=1):
+    """One launch of `walks_per_node` walks per node per rank on graph BG (weak)."""
+    torch = R.torch
+    import gwamd  # noqa: F401
+    from gwamd import _lib as C
+    from gwamd import dist as gdist
+    L = args.walk_length
+    world, rank = R.world, R.rank
+    bi = BG.info()
+    t0 = time.perf_counter()
+    bmode = "bitset"
+    try:
+        if force_rejection or (wp == 1.0 and wq == 1.0):
+            raise C.CapacityError(C.GW_ERR_CAPACITY, "rejection requested")
+        C.check(C.lib().gw_n2v_prepare(BG.handle, wp, wq, C.N2V_BITSET), BG.handle)
+    except C.CapacityError:
+        bmode = "rejection"
+        C.check(C.lib().gw_n2v_prepare(BG.handle, wp, wq, C.N2V_REJECTION), BG.handle)
+    torch.cuda.synchronize()
+    if wp == 1.0 and wq == 1.0:
+        bmode = "first-order"  # k_walk_scale<true,...>: no per-edge tables
+    bprep = time.perf_counter() - t0
+    nb = int(bi.n) * walks_per_node
+    bout = torch.empty((nb, L), dtype=torch.int32, device=R.dev)
+    bcnt = torch.zeros(2, dtype=torch.int64, device=R.dev)
+    stream = torch.cuda.current_stream(R.dev)
+    sh = C.ctypes.c_void_p(stream.cuda_stream)
 
-        ts_run(None)  # warm-up (also sizes the workspace)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t1 = time.perf_counter()
-        e0.record(stream)
-        ts_run(C.ptr(st))
-        e1.record(stream)
-        torch.cuda.synchronize()
-        tel = time.perf_counter() - t1
-        kt = e0.elapsed_time(e1) * 1e-3
-        if world > 1:
-            t = torch.tensor([tel], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            tel = float(t.item())
-            dist.all_reduce(st, op=dist.ReduceOp.SUM)
-        ext, upd = int(st[0].item()), int(st[1].item())
-        alg = (TOPSIM_B_EXT * ext + TOPSIM_B_UPD * upd) / max(world, 1)
-        cpu_ts = None
-        if rank == 0 and world == 1 and not args.no_cpu_baseline and name != "p10m":
-            cpu_ts = topsim_cpu_baseline(tg, sample, step, args)
-        return {
-            "metric": "SimRank pair-updates/sec (TopSim_singleSample)", "value": upd / tel,
-            "unit": "pair-updates/s", "path_extensions_per_s": ext / tel,
-            "config": {"workload": f"TopSim_singleSample on {name} ({desc}, Java multigraph), "
-                                   "all sources, replicated per rank",
-                       "step": step, "sample": sample, "C": 0.6, "topk": K},
-            "pair_updates": upd, "path_extensions": ext, "seconds": tel, "cpu_baseline": cpu_ts,
-            "roofline": {"bound": "hbm", "achieved": alg / kt / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": alg / kt / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": f"k_topsim<{step},*>", "kernel_ms": kt * 1e3},
-        }
+    def bstep(i, ev):
+        w0 = gdist.weak_block(i, world, rank, nb)
+        if ev is not None:
+            ev[0].record(stream)
+        C.check(C.lib().gw_n2v_walks(BG.handle, L, args.seed, w0, nb, 1, C.ptr(bout), None, C.ptr(bcnt), sh),
+                BG.handle)
+        if ev is not None:
+            ev[1].record(stream)
 
-    secondary = {}
-    if not args.no_topsim:
-        names = args.topsim_graphs.split(",")
-        res = [run_topsim(nm) for nm in names]
-        secondary["topsim"] = res[0]
-        if len(res) > 1:
-            secondary["topsim"]["more"] = res[1:]
+    bstep(0, None)
+    torch.cuda.synchronize()
+    bcnt.zero_()
+    sec, kms = time_steps(R, lambda i, ev: bstep(1 + i, ev), 1, 0)
+    bsteps = int(R.allreduce([int(bcnt[0].item())], "sum", torch.int64)[0])
+    local_steps = int(bcnt[0].item())
+    cpu_b = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_b = cpu_baseline_walks(BG.export_csr(), wp, wq, args.seed, L, 0, 10.0, max_walks=2_000_000)
+    del bout
+    return {"metric": f"walk-steps/sec (node2vec, {what})", "value": bsteps / sec, "unit": "walk-steps/s",
+            "n_ranks": world, "scaling": "weak",
+            "config": {"workload": f"node2vec p={wp} q={wq} on Graph500 R-MAT scale-{scale} ef {ef} "
+                                   f"(n={bi.n}, adjacency entries={bi.nnz}), walk_length={L}, "
+                                   f"{walks_per_node} walk(s)/node per rank", "sampler": bmode},
+            "kernel_ms": kms,
+            "roofline": {"bound": "hbm", "achieved": BYTES_PER_STEP * local_steps / (kms * 1e-3) / 1e9,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": BYTES_PER_STEP * local_steps / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "traffic": None, "kernel": "k_walk_bitset" if bmode == "bitset" else "k_walk_scale"},
+            "host_build_s": build_s, "prepare_s": bprep, "sampler_tables_gb": BG.info().sampler_bytes / 1e9,
+            "cpu_baseline": cpu_b}
 
-    # ---- naive SimRank (SimRank.java) on the GPU: the TopSim ground truth ----
-    def run_simrank(name):
-        from gwamd import topsim
+
+TOPSIM_GRAPHS = {"blog": ("blog.txt", 10313, ",", "lshrank blog, V=10313, 333,983 edges"),
+                 "arxiv": ("arxiv_author_pub.txt", 38741, "\t", "lshrank arxiv, V=38741, 58,595 edges"),
+                 "moreno": ("moreno_crime_crime.txt", 1380, "\t", "lshrank moreno, V=1380, 1,476 edges")}
+
+
+def topsim_roofline(ext, upd, kt, tag, nsrc):
+    """52 B per path extension + 24 B per pair-update / kernel time.
+    When the PMC traffic of this library build shows fewer HBM bytes than the
+    algorithmic count (cache-resident slot table and level records, LDS
+    accumulator), the bound is relabelled L2 and priced against 34.5 TB/s."""
+    alg = TOPSIM_B_EXT * ext + TOPSIM_B_UPD * upd
+    prof = load_prof(tag, nsrc, key="sources")
+    traffic = prof["hbm_bytes_per_launch"] if prof else None
+    achieved = alg / kt / 1e9
+    if traffic is not None and traffic >= alg:
+        bound, peak = "hbm", HBM_PEAK_GBS
+    elif traffic is not None:
+        bound, peak = "l2", L2_PEAK_GBS
+    else:
+        bound, peak = "unmeasured (no PMC pass for this library build)", None
+    return {"bound": bound, "achieved": achieved, "peak": peak, "unit": "GB/s",
+            "frac": achieved / peak if peak else None, "traffic": traffic,
+            "traffic_GBps": traffic / kt / 1e9 if traffic else None,
+            "algorithmic_bytes": alg, "kernel": "k_topsim", "kernel_ms": kt * 1e3}
+
+
+def run_topsim(R, args, name):
+    """TopSim_singleSample: lshrank graphs (config 3; every rank all sources) or
+    P10M (config 5; sources split over ranks, strong scaling)."""
+    import numpy as np
+    torch = R.torch
+    import gwamd
+    from gwamd import _lib as C
+    from gwamd import dist as gdist
+    from gwamd import topsim
+    world, rank = R.world, R.rank
+    K, sample, step = 20, args.topsim_sample, args.topsim_step
+    offs = nbrs = None
+    if name == "p10m":
+        # config 5: 10M-vertex Java-semantics R-MAT (reference quadrant recursion),
+        # 1e8 generated lines, all non-isolated sources, top-100
+        t0 = time.perf_counter()
+        a, b, c = rmat_abc(args)
+        pg = gwamd.GWGraph.rmat_java(10_000_000, 100_000_000, a, b, c, args.seed)
+        csr = pg.export_csr()
+        offs, nbrs = csr["offsets"], csr["nbrs"]
+        deg = np.diff(offs)
+        log(f"[rank {rank}] p10m built in {time.perf_counter() - t0:.1f}s")
+        pg.to_device(R.dev.index)
+        h = pg.handle
+        srcs_all = np.nonzero(deg > 0)[0].astype(np.int32)
+        sb, sc_ = gdist.shard_range(len(srcs_all), world, rank)
+        srcs = srcs_all[sb:sb + sc_]
+        desc = f"10M vertices, 1e8 R-MAT lines, {len(srcs_all)} non-isolated sources split over {world} rank(s)"
+        K, sample, step = 100, 1000, 3
+        scaling = "strong"
+        keep = pg
+    else:
         fname, V, sep, desc = TOPSIM_GRAPHS[name]
         tg = topsim.Graph(os.path.join(ROOT, "tests", "golden", "data", fname), V, separator=sep,
-                          device=dev.index)
+                          device=R.dev.index)
         tg._ensure_device()
         h = tg._g.handle
-        rounds = args.simrank_rounds
-        S = torch.empty((V, V), dtype=torch.float64, device=dev)
-        C.check(C.lib().gw_simrank_naive(h, 0.6, rounds, C.ptr(S), sh), h)  # warm-up, workspace
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        C.check(C.lib().gw_simrank_naive(h, 0.6, rounds, C.ptr(S), sh), h)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        sec = e0.elapsed_time(e1) * 1e-3
-        deg = np.diff(tg._offs)
-        nnz = int(deg.sum())
-        m = int((deg > 0).sum())
-        # entry gathers of the two passes (pass 1: m*nnz, pass 2: rows j > i only)
-        tail = np.cumsum(deg[::-1])[::-1]  # entries of rows >= v
-        p2 = int(tail[1:][deg[:-1] > 0].sum())
-        gathers = rounds * (m * nnz + p2)
-        lds_peak = 128.0 / 8 * 256 * 2.4e9  # 8 B gathers at 128 B/clk/CU
-        java_pairs = (nnz * nnz - int((deg.astype(np.int64) ** 2).sum())) // 2
-        cpu_sr = None
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            import oracle
-            nth = min(16, os.cpu_count() or 1)
-            budget, acc, re_ = 1.2e11, 0, 1
-            suffix = nnz - np.cumsum(deg)
-            while re_ < V and acc < budget:
-                acc += int(deg[re_]) * int(suffix[re_])
-                re_ += 1
-            Sh = np.eye(V)
-            t0 = time.perf_counter()
-            _, pairs = oracle.simrank_round_rows(tg._offs, tg._nbrs, 0.6, Sh, 1, re_, nthreads=nth)
-            dt = time.perf_counter() - t0
-            cpu_sr = {"value": pairs / dt / java_pairs, "unit": "rounds/s", "cores": nth, "kind": "port",
-                      "sample": f"rows 1..{re_ - 1} of one round ({pairs} neighbour pairs, {dt:.1f} s), "
-                                f"oracle/oracle.c or_simrank_round_rows (SimRank.java loop order), "
-                                f"scaled by the round's {java_pairs} pairs"}
-        return {
-            "metric": "naive SimRank rounds/sec (SimRank.java)", "value": rounds / sec, "unit": "rounds/s",
-            "config": {"workload": f"SimRank(g).compute() on {name} ({desc}, Java multigraph)",
-                       "rounds": rounds, "C": 0.6, "dense_result": f"{V}x{V} fp64"},
-            "seconds": sec, "entry_gathers": gathers, "java_neighbour_pairs_per_round": java_pairs,
-            "roofline": {"bound": "lds", "achieved": gathers / sec, "peak": lds_peak, "unit": "gathers/s",
-                         "frac": gathers / sec / lds_peak, "traffic": None, "kernel": "k_sr_gather<true,*>"},
-            "cpu_baseline": cpu_sr,
-        }
+        offs, nbrs = tg._offs, tg._nbrs
+        srcs = np.arange(V, dtype=np.int32)
+        scaling = "weak"
+        keep = tg
+    nloc = len(srcs)
+    src = torch.as_tensor(srcs, device=R.dev)
+    ids = torch.empty((max(nloc, 1), K), dtype=torch.int32, device=R.dev)
+    sc = torch.empty((max(nloc, 1), K), dtype=torch.float64, device=R.dev)
+    st = torch.zeros(4, dtype=torch.int64, device=R.dev)
+    stream = torch.cuda.current_stream(R.dev)
+    sh = C.ctypes.c_void_p(stream.cuda_stream)
 
-    # ---- north_star: walks on a ~10M-node / ~100M-edge power-law graph ----
-    def run_walk10m(BG, build_s, wp, wq, scale, ef, what="north_star 10M/100M graph", force_rejection=False):
-        bi = BG.info()
-        t0 = time.perf_counter()
-        bmode = "bitset"
-        try:
-            if force_rejection:
-                raise C.CapacityError(C.GW_ERR_CAPACITY, "rejection requested")
-            C.check(C.lib().gw_n2v_prepare(BG.handle, wp, wq, C.N2V_BITSET), BG.handle)
-        except C.CapacityError:
-            bmode = "rejection"
-            C.check(C.lib().gw_n2v_prepare(BG.handle, wp, wq, C.N2V_REJECTION), BG.handle)
-        torch.cuda.synchronize()
-        if wp == 1.0 and wq == 1.0:
-            bmode = "first-order"  # k_walk_scale<true,...>: no per-edge tables
-        bprep = time.perf_counter() - t0
-        bsampler_gb = BG.info().sampler_bytes / 1e9
-        nb = int(bi.n)
-        bout = torch.empty((nb, L), dtype=torch.int32, device=dev)
-        bcnt = torch.zeros(2, dtype=torch.int64, device=dev)
+    def ts_run(stats_ptr):
+        C.check(C.lib().gw_topsim(h, C.TOPSIM_SINGLE_SAMPLE, sample, step, 0.6, args.seed, C.ptr(src), nloc, K,
+                                  C.ptr(ids), C.ptr(sc), stats_ptr, sh), h)
 
-        def bstep(i):
-            w0 = gdist.weak_block(i, world, rank, nb)
-            C.check(C.lib().gw_n2v_walks(BG.handle, L, args.seed, w0, nb, 1, C.ptr(bout), None, C.ptr(bcnt), sh),
-                    BG.handle)
-        bstep(0)
-        torch.cuda.synchronize()
-        bcnt.zero_()
-        if world > 1:
-            dist.barrier()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t1 = time.perf_counter()
-        e0.record(stream)
-        bstep(1)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        sec = time.perf_counter() - t1
-        bsteps = int(bcnt[0].item())
-        if world > 1:
-            tt = torch.tensor([sec], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            sec = float(tt.item())
-            ss = torch.tensor([bsteps], dtype=torch.int64, device=dev)
-            dist.all_reduce(ss, op=dist.ReduceOp.SUM)
-            bsteps = int(ss.item())
-        kms = e0.elapsed_time(e1)
-        cpu_b = None
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            import oracle
-            csr_b = BG.export_csr()
-            nth = min(16, os.cpu_count() or 1)
-            # the CPU restatement of the rejection sampler (same walk distribution): the oracle's
-            # bitset restatement rebuilds each bitset per step and is no fair CPU baseline
-            fn = lambda c, *a, **k: oracle.walks_scale(dict(c, weights=None), *a, **k)  # noqa: E731
-            nw = 2000
-            t2 = time.perf_counter()
-            fn(csr_b, wp, wq, args.seed, L, 0, nw, nthreads=nth)
-            dt = time.perf_counter() - t2
-            if dt < 5.0:  # grow the sample to ~10 s of CPU work (first-order walks are cheap: cap it)
-                nw = int(nw * min(1000.0, 10.0 / max(dt, 1e-3)))
-                t2 = time.perf_counter()
-                fn(csr_b, wp, wq, args.seed, L, 0, nw, nthreads=nth)
-                dt = time.perf_counter() - t2
-            cpu_b = {"value": nw * (L - 1) / dt, "unit": "walk-steps/s", "cores": nth, "kind": "port",
-                     "sample": f"{nw} walks of the same graph, p and q, oracle/oracle.c or_walks_scale "
-                               f"(rejection sampler), {dt:.1f} s",
-                     "reference_python_context": "the reference node2vec.py cannot build per-edge alias tables "
-                                                 "for this graph (sum(deg^2) entries); SURVEY §6 measured "
-                                                 "4.1e4-3.7e5 walk-steps/s/core on small graphs"}
-        del bout
-        return {"metric": f"walk-steps/sec (node2vec, {what})", "value": bsteps / sec,
-                "unit": "walk-steps/s",
-                "config": {"workload": f"node2vec p={wp} q={wq} on Graph500 R-MAT scale-{scale} "
-                                       f"ef {ef} (n={bi.n}, adjacency entries={bi.nnz}), "
-                                       f"walk_length={L}, 1 walk/node per rank",
-                           "sampler": bmode},
-                "kernel_ms": kms, "host_build_s": build_s, "prepare_s": bprep, "sampler_tables_gb": bsampler_gb,
-                "cpu_baseline": cpu_b}
+    ts_run(None)  # warm-up (also sizes the workspace)
+    torch.cuda.synchronize()
 
-    if not args.no_walk10m:
-        t0 = time.perf_counter()
-        BG = gwamd.GWGraph.rmat(args.walk10m_scale, args.walk10m_edge_factor, 0.57, 0.19, 0.19, args.seed + 1)
-        build_s = time.perf_counter() - t0
-        BG.to_device(dev.index)
-        # the bench's p/q, then p=q=1 (the north_star graph walked first-order)
-        sc, ef = args.walk10m_scale, args.walk10m_edge_factor
-        secondary["walk_10m"] = run_walk10m(BG, build_s, args.p, args.q, sc, ef)
-        secondary["walk_10m_p1q1"] = run_walk10m(BG, build_s, 1.0, 1.0, sc, ef)
-        BG.free()
-
-    if not args.no_rmat24:
-        # config 4 on one GPU: R-MAT-24 ef 16, p=1 q=0.5 (bitset tables would need ~390 GB:
-        # rejection sampler with slot entries and per-row neighbour hash sets)
-        t0 = time.perf_counter()
-        BG = gwamd.GWGraph.rmat(24, 16, 0.57, 0.19, 0.19, args.seed)
-        build_s = time.perf_counter() - t0
-        BG.to_device(dev.index)
-        secondary["walk_rmat24_p1q05"] = run_walk10m(BG, build_s, 1.0, 0.5, 24, 16, "config 4 R-MAT-24 ef 16",
-                                                     force_rejection=True)
-        BG.free()
-
-    if not args.no_simrank:
-        sr = run_simrank(args.simrank_graph)
-        secondary["simrank_naive"] = sr
-
-    cpu = None
+    def tstep(i, ev):
+        if ev is not None:
+            ev[0].record(stream)
+        ts_run(C.ptr(st))
+        if ev is not None:
+            ev[1].record(stream)
+    tel, kms = time_steps(R, tstep, 1, 0)
+    ext_l, upd_l = int(st[0].item()), int(st[1].item())
+    ext, upd = (int(x) for x in R.allreduce([ext_l, upd_l], "sum", torch.int64))
+    tag = f"topsim_{name}_s{sample}_t{step}_k{K}"
+    cpu_ts = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(G.export_csr(), args, 0)
+        cpu_ts = cpu_baseline_topsim(offs, nbrs, len(offs) - 1, sample, step, args.seed,
+                                     args.cpu_seconds if name != "p10m" else 15.0, sources=srcs)
+    del keep
+    return {
+        "metric": "SimRank pair-updates/sec (TopSim_singleSample)", "value": upd / tel,
+        "unit": "pair-updates/s", "path_extensions_per_s": ext / tel, "n_ranks": world, "scaling": scaling,
+        "config": {"workload": f"TopSim_singleSample on {name} ({desc}, Java multigraph)",
+                   "step": step, "sample": sample, "C": 0.6, "topk": K},
+        "pair_updates": upd, "path_extensions": ext, "seconds": tel, "cpu_baseline": cpu_ts,
+        "roofline": topsim_roofline(ext_l, upd_l, kms * 1e-3, tag, nloc),
+    }
 
-    if rank == 0:
+
+def run_simrank(R, args, name):
+    """naive SimRank (SimRank.java) on the GPU: the TopSim ground truth."""
+    import numpy as np
+    torch = R.torch
+    from gwamd import _lib as C
+    from gwamd import topsim
+    fname, V, sep, desc = TOPSIM_GRAPHS[name]
+    tg = topsim.Graph(os.path.join(ROOT, "tests", "golden", "data", fname), V, separator=sep, device=R.dev.index)
+    tg._ensure_device()
+    h = tg._g.handle
+    rounds = args.simrank_rounds
+    S = torch.empty((V, V), dtype=torch.float64, device=R.dev)
+    stream = torch.cuda.current_stream(R.dev)
+    sh = C.ctypes.c_void_p(stream.cuda_stream)
+    C.check(C.lib().gw_simrank_naive(h, 0.6, rounds, C.ptr(S), sh), h)  # warm-up, workspace
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    C.check(C.lib().gw_simrank_naive(h, 0.6, rounds, C.ptr(S), sh), h)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    sec = e0.elapsed_time(e1) * 1e-3
+    deg = np.diff(tg._offs)
+    nnz = int(deg.sum())
+    m = int((deg > 0).sum())
+    tail = np.cumsum(deg[::-1])[::-1]  # entries of rows >= v
+    p2 = int(tail[1:][deg[:-1] > 0].sum())
+    gathers = rounds * (m * nnz + p2)  # entry gathers of the two passes (pass 2: rows j > i only)
+    lds_peak = 128.0 / 8 * 256 * 2.4e9  # 8 B gathers at 128 B/clk/CU
+    java_pairs = (nnz * nnz - int((deg.astype(np.int64) ** 2).sum())) // 2
+    cpu_sr = None
+    if R.rank == 0 and R.world == 1 and not args.no_cpu_baseline:
+        import oracle
+        nth = cores_used()
+        budget, acc, re_ = 1.2e11, 0, 1
+        suffix = nnz - np.cumsum(deg)
+        while re_ < V and acc < budget:
+            acc += int(deg[re_]) * int(suffix[re_])
+            re_ += 1
+        Sh = np.eye(V)
+        t0 = time.perf_counter()
+        _, pairs = oracle.simrank_round_rows(tg._offs, tg._nbrs, 0.6, Sh, 1, re_, nthreads=nth)
+        dt = time.perf_counter() - t0
+        cpu_sr = {"value": pairs / dt / java_pairs, "unit": "rounds/s", "cores": nth, "kind": "port",
+                  "sample": f"rows 1..{re_ - 1} of one round ({pairs} neighbour pairs, {dt:.1f} s), "
+                            f"oracle/oracle.c or_simrank_round_rows (SimRank.java loop order), "
+                            f"scaled by the round's {java_pairs} pairs"}
+    return {
+        "metric": "naive SimRank rounds/sec (SimRank.java)", "value": rounds / sec, "unit": "rounds/s",
+        "config": {"workload": f"SimRank(g).compute() on {name} ({desc}, Java multigraph)",
+                   "rounds": rounds, "C": 0.6, "dense_result": f"{V}x{V} fp64"},
+        "seconds": sec, "entry_gathers": gathers, "java_neighbour_pairs_per_round": java_pairs,
+        "roofline": {"bound": "lds", "achieved": gathers / sec, "peak": lds_peak, "unit": "gathers/s",
+                     "frac": gathers / sec / lds_peak, "traffic": None, "kernel": "k_sr_gather<true,*>"},
+        "cpu_baseline": cpu_sr,
+    }
+
+
+def run_arxiv(R, args):
+    """node2vec on lshrank arxiv (p=0.25, q=4, L=80, 10 walks/node): the graph on
+    which the reference node2vec.py itself was timed (profiles/
+    cpu_reference_node2vec.json), so GPU and reference share a workload."""
+    torch = R.torch
+    import gwamd
+    from gwamd import _lib as C
+    G = gwamd.GWGraph.from_edgelist(os.path.join(ROOT, "tests", "golden", "data", "arxiv_author_pub.txt"),
+                                    "\t", "nx").to_device(R.dev.index)
+    p, q, L, r = 0.25, 4.0, args.walk_length, 10
+    C.check(C.lib().gw_n2v_prepare(G.handle, p, q, C.N2V_BITSET), G.handle)
+    n = G.info().n
+    B = r * n
+    out = torch.empty((B, L), dtype=torch.int32, device=R.dev)
+    cnt = torch.zeros(2, dtype=torch.int64, device=R.dev)
+    stream = torch.cuda.current_stream(R.dev)
+    sh = C.ctypes.c_void_p(stream.cuda_stream)
+
+    def st(i, ev):
+        if ev is not None:
+            ev[0].record(stream)
+        C.check(C.lib().gw_n2v_walks(G.handle, L, args.seed, i * B, B, 1, C.ptr(out), None, C.ptr(cnt), sh),
+                G.handle)
+        if ev is not None:
+            ev[1].record(stream)
+    st(0, None)
+    torch.cuda.synchronize()
+    cnt.zero_()
+    sec, kms = time_steps(R, lambda i, ev: st(1 + i, ev), 3, 0)
+    steps = int(cnt[0].item())
+    ref = reference_cpu_fixture()
+    refline = None
+    if ref:
+        for e in ref.get("graphs", []):
+            if e.get("graph") == "arxiv" and e.get("p") == p and e.get("q") == q:
+                refline = {"value": e["walk_steps_per_s_1proc"], "unit": "walk-steps/s", "cores": 1,
+                           "kind": "reference", "sample": e.get("sample"), "cpu_model": ref.get("cpu_model"),
+                           "value_8proc": e.get("walk_steps_per_s_8proc"),
+                           "source": "profiles/cpu_reference_node2vec.json (reference node2vec.py timed in the "
+                                     "build container: it cannot travel to the GPU box)"}
+    G.free()
+    return {"metric": "walk-steps/sec (node2vec, lshrank arxiv)", "value": steps / sec, "unit": "walk-steps/s",
+            "config": {"workload": f"node2vec p={p} q={q} on lshrank arxiv_author_pub (nx semantics, n={n}), "
+                                   f"walk_length={L}, {r} walks/node", "sampler": "bitset"},
+            "kernel_ms": kms, "cpu_baseline": refline}
+
+
+def main(argv):
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        return launch_ranks(args, argv)
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+        return 2
+    R = Ranks(args)
+    secondary = {}
+    cpu = None
+    if args.config == 5:
+        if R.plumbing:
+            raise SystemExit("--plumbing-check covers configs 2 and 4")
+        h = run_topsim(R, args, "p10m")
+        value, metric, unit = h["value"], h["metric"], h["unit"]
+        head = h
+    else:
+        head = walk_headline(R, args)
+        value, metric, unit = head["value"], "walk-steps/sec (node2vec)", "walk-steps/s"
+        cpu = head.get("cpu_baseline")
+    sec_mode = args.secondary
+    if not R.plumbing and sec_mode != "none" and args.config == 2:
+        if R.world == 1 or sec_mode == "all":
+            if not args.no_topsim:
+                res = [run_topsim(R, args, nm) for nm in args.topsim_graphs.split(",")]
+                secondary["topsim"] = res[0]
+                if len(res) > 1:
+                    secondary["topsim"]["more"] = res[1:]
+            if not args.no_arxiv:
+                secondary["walk_arxiv"] = run_arxiv(R, args)
+            if not args.no_walk10m:
+                t0 = time.perf_counter()
+                a, b, c = rmat_abc(args)
+                BG = gwamd_graph_rmat(args.walk10m_scale, args.walk10m_edge_factor, a, b, c, args.seed + 1)
+                build_s = time.perf_counter() - t0
+                BG.to_device(R.dev.index)
+                sc, ef = args.walk10m_scale, args.walk10m_edge_factor
+                secondary["walk_10m"] = walk_secondary(R, args, BG, build_s, args.p, args.q, sc, ef,
+                                                       "north_star 10M/100M graph")
+                secondary["walk_10m_p1q1"] = walk_secondary(R, args, BG, build_s, 1.0, 1.0, sc, ef,
+                                                            "north_star 10M/100M graph")
+                BG.free()
+            if not args.no_simrank:
+                secondary["simrank_naive"] = run_simrank(R, args, args.simrank_graph)
+        if not args.no_rmat24:
+            # config 4: R-MAT-24 ef 16, p=1 q=0.5 (bitset tables would need ~390 GB: rejection
+            # sampler with slot entries and per-row neighbour hash sets); 1 walk/node per rank
+            t0 = time.perf_counter()
+            a, b, c = rmat_abc(args)
+            BG = gwamd_graph_rmat(24, 16, a, b, c, args.seed)
+            build_s = time.perf_counter() - t0
+            BG.to_device(R.dev.index)
+            secondary["walk_rmat24_p1q05"] = walk_secondary(R, args, BG, build_s, 1.0, 0.5, 24, 16,
+                                                            "config 4 R-MAT-24 ef 16", force_rejection=True)
+            BG.free()
+        if not args.no_p10m:
+            secondary["topsim_p10m"] = run_topsim(R, args, "p10m")
+    if R.rank == 0:
+        ngpu = R.ngpu
         res = {
-            "metric": "walk-steps/sec (node2vec)",
+            "metric": metric,
             "value": value,
-            "unit": "walk-steps/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": el / args.steps * 1e3,
+            "unit": unit,
+            "n_gpus": ngpu,
+            "ranks": R.world,
+            "steps": args.steps if args.config != 5 else 1,
+            "warmup": args.warmup if args.config != 5 else 1,
+            "ms_per_step": head["seconds"] / (args.steps if args.config != 5 else 1) * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.config != 5 else "strong",
             "vs_baseline": None,
-            "dtype": "int32 ids / f64 accept tests",
-            "data": "synthetic",
-            "config": {"workload": f"node2vec p={args.p} q={args.q} on synthetic Graph500 R-MAT scale-{args.scale} "
-                                   f"(ef {args.edge_factor}, a,b,c=0.57,0.19,0.19, seed {args.seed}; n={n}, "
-                                   f"adjacency entries={nnz}), walk_length={L}, {args.num_walks} walks/node per "
-                                   f"rank per step",
-                       "walks_per_step": B * world, "walk_length": L, "parallelism": f"replicated graph, walks sharded over {world} rank(s)",
-                       "allgather": bool(gather is not None)},
-            "walk_steps": steps_total,
-            "sampler": mode, "prepare_seconds": prep_s, "sampler_tables_gb": sampler_gb,
-            "rejection_trials_per_step": trials_total / max(steps_total, 1),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_walk_bitset" if mode == "bitset" else "k_walk_scale<false,false,false>",
-                         "kernel_ms": k_avg_ms,
-                         "bytes_per_unit": BYTES_PER_STEP, "units_per_launch": launch_steps,
-                         "lib_sha256": lib_digest(), "random_line_roofline": line_rate},
-            "cpu_baseline": cpu,
-            "secondary": secondary or None,
+            "dtype": "int32 ids / f64 accept tests" if args.config != 5 else "f64 scores / int32 ids",
+            "data": "synthetic" if not R.plumbing else "plumbing-check: synthetic rows, no GPU work",
+            "backend": R.backend,
         }
+        if R.world > 1 and R.ngpu < R.world:
+            res["rehearsal"] = f"{R.world} ranks share {R.ngpu} GPU(s): not a scaling measurement"
+        if args.config == 5:
+            res["config"] = dict(head["config"], parallelism=f"replicated graph, sources split over {R.world} rank(s)")
+            res["roofline"] = head["roofline"]
+            res["cpu_baseline"] = head["cpu_baseline"]
+            res["pair_updates"] = head["pair_updates"]
+        else:
+            a, b, c = rmat_abc(args)
+            res["config"] = {
+                "workload": f"node2vec p={args.p} q={args.q} on synthetic R-MAT scale-{args.scale} (ef "
+                            f"{args.edge_factor}, a,b,c={a},{b},{c}, seed {args.seed}; n={head['n']}, "
+                            f"adjacency entries={head['nnz']}), walk_length={args.walk_length}, "
+                            f"{args.num_walks} walks/node per rank per step",
+                "baseline_config": args.config,
+                "walks_per_step": head["B"] * R.world, "walk_length": args.walk_length,
+                "parallelism": f"replicated graph, walks sharded over {R.world} rank(s)"}
+            res["walk_steps"] = head["walk_steps"]
+            for k in ("mode", "prep_s", "sampler_gb", "trials_per_step"):
+                if k in head:
+                    res[{"mode": "sampler", "prep_s": "prepare_seconds", "sampler_gb": "sampler_tables_gb",
+                         "trials_per_step": "rejection_trials_per_step"}[k]] = head[k]
+            res["roofline"] = head.get("roofline")
+            res["cpu_baseline"] = cpu
+            if "allgather" in head:
+                res["allgather"] = head["allgather"]
+                res["allgather_all_ranks_ok"] = head["allgather_all_ranks_ok"]
+        ref = reference_cpu_fixture()
+        if ref and not R.plumbing:
+            res["reference_cpu_context"] = {"file": "profiles/cpu_reference_node2vec.json",
+                                            "summary": ref.get("summary")}
+        res["secondary"] = secondary or None
         print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    R.close()
+    return 0
+
+
+def gwamd_graph_rmat(scale, ef, a, b, c, seed):
+    import gwamd
+    return gwamd.GWGraph.rmat(scale, ef, a, b, c, seed)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main(sys.argv[1:]))

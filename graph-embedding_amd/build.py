@@ -54,7 +54,14 @@ def _run(cmd, verbose):
     return r
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, diag=False):
+    """diag=True: the timing-experiment build (-DGW_DIAG: GW_DIAG_* knobs, some of
+    which return wrong walks on purpose) into gwamd/libgraphwalk_diag.so; the
+    release library never carries those paths."""
+    BUILD = os.path.join(HERE, "build_diag" if diag else "build")
+    OUT = os.path.join(HERE, "gwamd", "libgraphwalk_diag.so" if diag else "libgraphwalk.so")
+    hip_flags = HIPCC_FLAGS + (["-DGW_DIAG"] if diag else [])
+    cxx_flags = CXX_FLAGS + (["-DGW_DIAG"] if diag else [])
     os.makedirs(BUILD, exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "graphwalk.h")]
     jobs = []
@@ -65,20 +72,22 @@ def build(force=False, verbose=False):
         obj = os.path.join(BUILD, s + ".o")
         objs.append(obj)
         if force or _newer(obj, [src] + hdrs + [__file__]):
-            jobs.append([hipcc] + HIPCC_FLAGS + ["-c", src, "-o", obj])
+            jobs.append([hipcc] + hip_flags + ["-c", src, "-o", obj])
     cxx = shutil.which("g++") or "g++"
     for s in CXX_SRCS:
         src = os.path.join(CSRC, s)
         obj = os.path.join(BUILD, s + ".o")
         objs.append(obj)
         if force or _newer(obj, [src] + hdrs + [__file__]):
-            jobs.append([cxx] + CXX_FLAGS + ["-c", src, "-o", obj])
+            jobs.append([cxx] + cxx_flags + ["-c", src, "-o", obj])
     with cf.ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         list(ex.map(lambda c: _run(c, verbose), jobs))
     if force or jobs or _newer(OUT, objs):
         _run([cxx, "-shared", "-o", OUT] + objs +
              [f"-L{ROCM}/lib", "-lamdhip64", "-fopenmp", "-ldl", f"-Wl,-rpath,{ROCM}/lib",
               "-Wl,--no-undefined"], verbose)
+    if diag:
+        return OUT
     # C++ host mirror of the Java TopSim API + the benchmark driver binary
     host = os.path.join(HERE, "host")
     bindir = os.path.join(HERE, "bin")
@@ -99,5 +108,6 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--diag", action="store_true", help="timing-experiment library (-DGW_DIAG)")
     a = ap.parse_args()
-    print(build(force=a.force, verbose=a.verbose))
+    print(build(force=a.force, verbose=a.verbose, diag=a.diag))

@@ -8,6 +8,19 @@
 
 #include "../../include/graphwalk.h"
 
+// Diagnostic A/B knobs (timing experiments; some of them return wrong walks on
+// purpose) exist only in libraries built with -DGW_DIAG (build.py --diag writes
+// gwamd/libgraphwalk_diag.so, loaded with GW_LIB=...): the release library
+// neither reads the GW_DIAG_* variables nor carries their code paths.
+#ifdef GW_DIAG
+#include <cstdlib>
+constexpr bool kGwDiag = true;
+#define GW_DIAG_ENV(name) std::getenv(name)
+#else
+constexpr bool kGwDiag = false;
+#define GW_DIAG_ENV(name) ((const char*)nullptr)
+#endif
+
 // Device-side mirror of the CSR (all pointers are HBM allocations owned by
 // the handle).  Layout (SoA, one array per field so each gather touches only
 // the bytes it needs):

@@ -460,7 +460,7 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
     // sectors instead of a 16 B piece of 64 (per-lane stores cost up to 22%
     // of a launch: GW_DIAG_NO_STORE A/B)
     const unsigned long long rm = __ballot(ready);
-    if (rm && !P.diag) {
+    if (rm && !(kGwDiag && P.diag)) {
       if (vec_ok) {
         __builtin_amdgcn_wave_barrier();
         const int32_t* sw = &s_stage[threadIdx.x >> 6][0][0];
@@ -652,8 +652,8 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
   dev_free(d.eh);
   gw_dev_bitset_release(g);
   g->bitset_words = 0;
-  const char* nobm = getenv("GW_DIAG_NO_BITMAP");  // diagnostic A/B knob only
-  const char* noeh = getenv("GW_DIAG_NO_EHASH");   // diagnostic A/B knob only
+  const char* nobm = GW_DIAG_ENV("GW_DIAG_NO_BITMAP");  // diagnostic A/B knob only
+  const char* noeh = GW_DIAG_ENV("GW_DIAG_NO_EHASH");   // diagnostic A/B knob only
   if (mode == GW_N2V_REJECTION && !(p == 1.0 && q == 1.0) && g->nnz && g->semantics == GW_SEM_NX_SIMPLE &&
       !(noeh && noeh[0] == '1')) {
     size_t fr = 0, tot = 0;
@@ -681,7 +681,7 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
   }
   dev_free(d.sent);
   const bool fo = (p == 1.0 && q == 1.0);
-  const char* nosent = getenv("GW_DIAG_NO_SENT");  // diagnostic A/B knob only
+  const char* nosent = GW_DIAG_ENV("GW_DIAG_NO_SENT");  // diagnostic A/B knob only
   if ((mode == GW_N2V_REJECTION || fo) && g->nnz && !(nosent && nosent[0] == '1')) {
     // slot entries (16 B per slot, one dwordx4 per step) spare the candidate's
     // offsets[] read: +14% on R-MAT-24 ef 16 (p=1, q=0.5; 8.3 GB of entries),
@@ -864,7 +864,7 @@ int gw_dev_n2v_walks(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int6
   P.pk0 = (uint32_t)seed;
   P.pk1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_PERM;
   {
-    const char* ns = getenv("GW_DIAG_NO_STORE");
+    const char* ns = GW_DIAG_ENV("GW_DIAG_NO_STORE");
     P.diag = (ns && ns[0] == '1') ? 1u : 0u;
   }
   if (g->n2v_mode == GW_N2V_BITSET && !first_order)

@@ -736,7 +736,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
             op = 2;
           }
         }
-        if (P.diag) {  // timing experiments only
+        if (kGwDiag && P.diag) {  // timing experiments only (-DGW_DIAG builds)
           if (op == 1 && (P.diag & 1)) {
             k = (int64_t)((uint64_t)j * (uint64_t)d / c);
             acc = true;
@@ -802,7 +802,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
           } else if (mode == BS_REGION && k != (int64_t)kp && trial < (1u << 24)) {
             const uint32_t fb = gw_bounded(u.y, bs_filt_buckets(ndir));
             if ((pick10(pl, bs_filt_word(ndir) + (fb >> 5)) >> (fb & 31)) & 1u) {  // maybe common: read the word
-              sw = (P.diag & 8) ? G.bs_region[((uint32_t)k >> 5) & 0xFFFFu]  // timing experiment: no TLB misses
+              sw = (kGwDiag && (P.diag & 8)) ? G.bs_region[((uint32_t)k >> 5) & 0xFFFFu]  // timing experiment: no TLB misses
                                 : hreg[(meta >> 16) * kBlk + (k >> 5)];
               sbit = (uint32_t)(k & 31);
               spec = true;
@@ -812,7 +812,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
         }
       }
       if (ph == 2 && !acc) {  // fetch the region block (this iteration's round trip)
-        sec = (P.diag & 4) ? (uint64_t)(G.bs_region + kBlk * ((pl[0] + (uint32_t)g) & 0xFFFu))
+        sec = (kGwDiag && (P.diag & 4)) ? (uint64_t)(G.bs_region + kBlk * ((pl[0] + (uint32_t)g) & 0xFFFu))
                            : (uint64_t)(hreg + ((meta >> 16) + (uint32_t)g) * kBlk);
         isblk = true;
       }
@@ -873,7 +873,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
     // flush of the ready walkers' 64 B chunks, cooperative like the loads:
     // an instruction writes 16 whole sectors instead of a 16 B piece of 64
     const unsigned long long rm = __ballot(ready);
-    if (rm && !(P.diag & 32)) {
+    if (rm && !(kGwDiag && (P.diag & 32))) {
       if (vec_ok) {
         __builtin_amdgcn_wave_barrier();
         const int32_t* sw = &s_stage[wv][0][0];
@@ -1035,9 +1035,9 @@ int gw_dev_walk_bitset_launch(gw_graph* g, int L, uint64_t seed, int64_t walk_be
   P.k1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_STEP;
   P.pk0 = (uint32_t)seed;
   P.pk1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_PERM;
-  const char* dg = getenv("GW_DIAG_BS");  // diagnostic A/B knob only
+  const char* dg = GW_DIAG_ENV("GW_DIAG_BS");  // diagnostic A/B knob only
   P.diag = dg ? (uint32_t)atoi(dg) : 0u;
-  if (const char* ns = getenv("GW_DIAG_NO_STORE")) P.diag |= ns[0] == '1' ? 32u : 0u;
+  if (const char* ns = GW_DIAG_ENV("GW_DIAG_NO_STORE")) P.diag |= ns[0] == '1' ? 32u : 0u;
   const unsigned grid = (unsigned)std::max<int64_t>(1, (walk_count + kB - 1) / kB);
   k_walk_bitset<<<grid, kB, 0, (hipStream_t)stream>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev,
                                                        len_dev, (unsigned long long*)counters_dev);

@@ -353,8 +353,8 @@ int gw_dev_simrank_naive(gw_graph* g, double C, int iters, double* sim_dev, void
     GW_HIP_TRY(hipGetLastError());
     SrArgs A{m, g->sr_off, g->sr_ent, g->sr_heads, C};
     // input row in LDS when it leaves room for a window of SR_MIN_WIN rows;
-    // GW_DIAG_SR_GLOBAL_ROW=1 forces the HBM-row variant (tests compare the two)
-    const char* diag = std::getenv("GW_DIAG_SR_GLOBAL_ROW");
+    // GW_SIMRANK_HBM_ROW=1 selects the HBM-row variant (same bits; tests compare the two)
+    const char* diag = std::getenv("GW_SIMRANK_HBM_ROW");
     const int64_t cap = SR_LDS_BYTES / (int64_t)sizeof(double);
     const bool lds_row = m + SR_MIN_WIN <= cap && !(diag && diag[0] == '1');
     const int win = (int)std::min<int64_t>(m, lds_row ? cap - m : cap);

@@ -325,7 +325,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   if (tid == 0)
     for (int k = 0; k < 11; ++k) s_ph[k] = 0;
   auto mark = [&](int k) {
-    if (A.phase && tid == 0) {
+    if (kGwDiag && A.phase && tid == 0) {
       const unsigned long long now = __builtin_readcyclecounter();
       if (k >= 0) s_ph[k] += now - s_ph[10];
       s_ph[10] = now;
@@ -523,7 +523,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
               alive = false;
             } else {
               uint32_t ux;
-              if (A.diag & 2) {
+              if (kGwDiag && (A.diag & 2)) {
                 ux = ((uint32_t)s * 0x9E3779B1u) ^ ((uint32_t)g * 0x85EBCA6Bu) ^ ((uint32_t)t * 0xC2B2AE35u);
                 ux ^= ux >> 15;
                 ux *= 0x2C1B3C6Du;
@@ -536,7 +536,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
               dcur = e.d;
               ocur = e.off;
               ++my_ext;
-              if ((t & 1) == 0 && !(A.diag & 1)) contrib(path, dpath, t / 2, s, mw);
+              if ((t & 1) == 0 && !(kGwDiag && (A.diag & 1))) contrib(path, dpath, t / 2, s, mw);
             }
           }
         }
@@ -801,7 +801,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     mark(4);
   }
 
-  if (A.phase && tid == 0)
+  if (kGwDiag && A.phase && tid == 0)
     for (int k = 0; k < 10; ++k) atomicAdd(&A.phase[k], s_ph[k]);
   // statistics
   long long e = block_sum<long long>(my_ext, s_red);
@@ -944,7 +944,7 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   }
   bool lds_row = n * 8 <= LDS_ROW_MAX_BYTES;
   int mode = lds_row ? 0 : 2;
-  if (const char* hm = std::getenv("GW_DIAG_TS_HASH")) {  // A/B knob: force the 8192- (1) or 6144-slot (2) hash
+  if (const char* hm = GW_DIAG_ENV("GW_DIAG_TS_HASH")) {  // A/B knob: force the 8192- (1) or 6144-slot (2) hash
     if (hm[0] == '1' || hm[0] == '2') {
       mode = hm[0] - '0';
       lds_row = false;
@@ -1026,7 +1026,7 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   A.G = g->d;
   A.variant = variant;
   {
-    const char* dg = std::getenv("GW_DIAG_TS");
+    const char* dg = GW_DIAG_ENV("GW_DIAG_TS");
     A.diag = dg ? std::atoi(dg) : 0;
   }
   A.sample = sample;
@@ -1065,7 +1065,7 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   GW_HIP_TRY(hipMemsetAsync(t.error_flag, 0, sizeof(int), s));
   const int blocks = (int)std::min<int64_t>(t.blocks, nsrc);
   // GW_DIAG_TS_PHASES=1: cycles per kernel phase summed over blocks, to stderr (diagnostics only)
-  const char* dph = std::getenv("GW_DIAG_TS_PHASES");
+  const char* dph = GW_DIAG_ENV("GW_DIAG_TS_PHASES");
   A.phase = nullptr;
   if (dph && dph[0] == '1') {
     GW_HIP_TRY(hipMalloc((void**)&A.phase, 10 * sizeof(unsigned long long)));

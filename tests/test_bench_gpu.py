@@ -1,0 +1,57 @@
+"""GPU: bench.py end to end on small graphs — one rank, and two ranks on the
+one GPU of the test box over gloo (GW_DIST_BACKEND=gloo: RCCL refuses two ranks
+on one device), which exercises the launcher, the weak-scaling walk blocks, the
+max-over-ranks timing and the all-gather check with real HIP walks."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+BENCH = os.path.join(ROOT, "bench.py")
+SMALL = ["--scale", "12", "--steps", "2", "--warmup", "1", "--secondary", "none", "--no-cpu-baseline"]
+
+
+def _run(args, env_extra=None, timeout=300):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, "-u", BENCH] + args, capture_output=True, text=True, timeout=timeout,
+                       env=env, cwd=ROOT)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_one_rank_small():
+    rc, res, err = _run(SMALL)
+    assert rc == 0, err[-3000:]
+    assert res["n_gpus"] == 1 and res["ranks"] == 1 and res["value"] > 0
+    r = res["roofline"]
+    assert r["units_per_launch"] * 2 == res["walk_steps"]
+    assert r["random_line_roofline"]["calibrated_peak_lines_per_s"] > 1e10
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo_on_gpu():
+    rc, res, err = _run(["--gpus", "2"] + SMALL, {"GW_DIST_BACKEND": "gloo"})
+    assert rc == 0, err[-3000:]
+    assert res["ranks"] == 2 and res["n_gpus"] == 1 and "rehearsal" in res
+    n = int(res["config"]["walks_per_step"]) // 20  # 10 walks/node per rank, 2 ranks
+    # R-MAT is undirected with no isolated starts: every walk has all 80 positions
+    assert res["walk_steps"] == 2 * 2 * 10 * n * 79
+    assert res["allgather"]["check_last_rank_block_identical"] is True
+    assert res["allgather_all_ranks_ok"] is True
+
+
+@pytest.mark.gpu
+def test_bench_config4_shape_small():
+    # config 4's sampler and p/q (rejection, p=1, q=0.5) on a small R-MAT
+    rc, res, err = _run(["--config", "4"] + SMALL)
+    assert rc == 0, err[-3000:]
+    assert res["sampler"] == "rejection" and res["config"]["baseline_config"] == 4
+    assert res["value"] > 0 and 1.0 <= res["rejection_trials_per_step"] < 3.0

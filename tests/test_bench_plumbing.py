@@ -1,0 +1,52 @@
+"""CPU: bench.py's multi-rank path — `--gpus 2` launches two ranks
+through torch.distributed.run as a child process, the ranks meet over gloo,
+walk-step counts are summed over ranks, the max-over-ranks time is taken and
+the all-gather of the emitted rows is checked byte-for-byte on rank 0.  The
+rows are synthetic (`--plumbing-check`: no GPU here); the GPU test
+`test_n2v_gpu.py::test_bench_two_ranks_gloo_on_gpu` runs the same path with
+real walks."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(args, env_extra=None, timeout=240):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, timeout=timeout, env=env,
+                       cwd=ROOT)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+@pytest.mark.parametrize("limit", [None, 200_000])
+def test_bench_two_ranks_plumbing(limit):
+    steps, scale, L, nw = 3, 8, 80, 10
+    env = {"GW_BENCH_GATHER_LIMIT": str(limit)} if limit else None
+    rc, res, err = _run(["--gpus", "2", "--plumbing-check", "--scale", str(scale), "--steps", str(steps),
+                         "--warmup", "1"], env)
+    assert rc == 0, err[-2000:]
+    assert res["ranks"] == 2 and res["backend"] == "gloo"
+    assert res["n_gpus"] == 0 and "rehearsal" in res  # no GPU: never reported as a GPU count
+    B = nw * (1 << scale)
+    assert res["config"]["walks_per_step"] == 2 * B
+    assert res["walk_steps"] == 2 * steps * B * (L - 1)
+    g = res["allgather"]
+    assert g["check_last_rank_block_identical"] is True and res["allgather_all_ranks_ok"] is True
+    assert g["gathered_bytes_per_step_per_rank"] == B * L * 4
+    assert g["mode"] == ("whole" if limit is None else "ring of 312-row chunks")
+
+
+def test_bench_rank_count_mismatch_is_refused():
+    rc, res, err = _run(["--gpus", "2", "--plumbing-check"], {"WORLD_SIZE": "1"}, timeout=120)
+    assert rc == 2 and res is None
+    assert "WORLD_SIZE=1" in err

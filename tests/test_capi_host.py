@@ -272,3 +272,15 @@ def test_comm_argument_errors(gw):
     assert L.gw_comm_allgather(None, None, None, 4, 0, None) == C.GW_ERR_INVALID
     assert L.gw_comm_free(None) == C.GW_OK
     assert L.gw_comm_unique_id(None) == C.GW_ERR_INVALID
+
+
+def test_release_library_has_no_diagnostic_knobs(gw):
+    """The GW_DIAG_* timing knobs (some return wrong walks on purpose) are
+    compiled only into the -DGW_DIAG library (build.py --diag): the release
+    libgraphwalk.so neither names nor reads them."""
+    from gwamd import _lib
+    if os.path.basename(_lib.LIB_PATH) != "libgraphwalk.so":
+        pytest.skip("GW_LIB points at a non-release library")
+    with open(_lib.LIB_PATH, "rb") as f:
+        blob = f.read()
+    assert b"GW_DIAG" not in blob

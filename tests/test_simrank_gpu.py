@@ -63,7 +63,7 @@ def test_naive_simrank_global_row_path_bitwise(gw, monkeypatch):
     LDS-row variant (same reduction order)."""
     g = _graph("moreno")
     a = _gpu(g, 0.6, 3)
-    monkeypatch.setenv("GW_DIAG_SR_GLOBAL_ROW", "1")
+    monkeypatch.setenv("GW_SIMRANK_HBM_ROW", "1")
     b = _gpu(g, 0.6, 3)
     assert np.array_equal(a, b)
 
