@@ -211,8 +211,8 @@ struct N2VParams {
 
 template <bool WEIGHTED>
 __device__ __forceinline__ int64_t draw_first_order(const gw_dev_graph& G, int64_t b,
-                                                    int64_t d, uint32_t ux, uint32_t uy) {
-  int64_t kk = (int64_t)gw_bounded(ux, (uint32_t)d);
+                                                    int64_t d, uint32_t ux, uint32_t ulo, uint32_t uy) {
+  int64_t kk = (int64_t)gw_index(ux, ulo, (uint32_t)d);  // 64-bit draw (ux:ulo)
   if (!WEIGHTED) return kk;
   return (gw_u01(uy) < G.node_q[b + kk]) ? kk : (int64_t)G.node_J[b + kk];
 }
@@ -366,7 +366,7 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
       if (FIRST_ORDER || len == 1) {
         gw_u4 u = gw_philox(c0, c1, (uint32_t)len, 0u, P.k0, P.k1);
         trial = 1;
-        slot = b + draw_first_order<WEIGHTED>(G, b, d, u.x, u.y);
+        slot = b + draw_first_order<WEIGHTED>(G, b, d, u.x, u.z, u.y);
         if (FIRST_ORDER && ENT) {  // the slot entry carries the next row
           const gw_ts_ent en = gw_ts_load(G.sent + slot);
           next = en.x;
@@ -386,7 +386,11 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
           next = prev;
           acc = true;
         } else {
-          slot = b + draw_first_order<WEIGHTED>(G, b, d, u.x, u.y);
+          // low word of the index draw: u.y (unweighted), else one more Philox block
+          // (u.y is the weighted node-alias accept, u.z / u.w are taken)
+          const uint32_t ulo =
+              WEIGHTED ? gw_philox(c0, c1, (uint32_t)len, (trial - 1u) | 0x80000000u, P.k0, P.k1).x : u.y;
+          slot = b + draw_first_order<WEIGHTED>(G, b, d, u.x, ulo, u.y);
           if (ENT) {  // the slot entry carries the candidate's row for the next step
             const gw_ts_ent en = gw_ts_load(G.sent + slot);
             next = en.x;

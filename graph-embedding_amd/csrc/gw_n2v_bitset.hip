@@ -263,8 +263,9 @@ struct BsEmit {
     } else {
       atomicOr(&bits[k >> 5], bit);
       set_dir((kprev < 0 ? -1 : kprev / kDirBits) + 1, k / kDirBits, idx);
-      // filter: the draws u with floor(u*d / 2^32) == k span at most two buckets
-      const uint64_t ulo = (((uint64_t)k << 32) + d - 1) / d;
+      // filter over the draw's high word y (bucket floor(y*F / 2^32)): the 64-bit draws
+      // (y:z) with index k have y in [floor(k*2^32/d), ceil((k+1)*2^32/d) - 1]
+      const uint64_t ulo = ((uint64_t)k << 32) / d;
       const uint64_t uhi = ((((uint64_t)k + 1) << 32) + d - 1) / d - 1;
       const uint32_t F = bs_filt_buckets(ndir), w0 = bs_filt_word(ndir);
       const uint32_t b0 = gw_bounded((uint32_t)ulo, F), b1 = gw_bounded((uint32_t)uhi, F);
@@ -713,7 +714,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
         int op = 0;  // 1: the j-th common position; 2: is draw k common
         uint32_t j = 0;
         if (len == 1) {
-          k = (int64_t)gw_bounded(u.x, d);
+          k = (int64_t)gw_index(u.x, u.z, d);
           acc = true;
         } else {
           bool other = trial > 1;  // a retry is always the "other" branch
@@ -732,7 +733,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
             }
           }
           if (other) {
-            k = (int64_t)gw_bounded(u.y, d);
+            k = (int64_t)gw_index(u.y, u.z, d);
             op = 2;
           }
         }

@@ -66,10 +66,19 @@ GW_HD struct gw_u4 gw_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
 // u32 -> [0,1) double with 32 random bits (exact: x * 2^-32).
 GW_HD double gw_u01(uint32_t x) { return (double)x * 2.3283064365386963e-10; }
 
-// Uniform index in [0, d): Lemire multiply-high (bias <= d / 2^32, documented;
-// identical on host and device so parity is bitwise).
+// Bucket in [0, d) of a 32-bit draw: multiply-high (relative bias <= d / 2^32).
+// Used for the small fixed bucket counts of the walk kernels' draw filters.
 GW_HD uint32_t gw_bounded(uint32_t x, uint32_t d) {
   return (uint32_t)(((uint64_t)x * (uint64_t)d) >> 32);
+}
+
+// Uniform index in [0, d) of a 64-bit draw v = hi * 2^32 + lo: floor(v * d / 2^64),
+// exactly (hi*d + floor(lo*d / 2^32) < 2^64 and its floor / 2^32 equals the full
+// product's).  Relative bias <= d / 2^64, below the reference's floor(U*K) with
+// a 53-bit U (node2vec.py:157, K / 2^53) for every d < 2^32.  Every neighbour
+// index draw uses it; identical on host and device so parity is bitwise.
+GW_HD uint32_t gw_index(uint32_t hi, uint32_t lo, uint32_t d) {
+  return (uint32_t)(((uint64_t)hi * (uint64_t)d + (((uint64_t)lo * (uint64_t)d) >> 32)) >> 32);
 }
 
 // Keyed bijection on [0, n) (n < 2^62): a 4-round Feistel network over the

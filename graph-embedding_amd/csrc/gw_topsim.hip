@@ -522,15 +522,17 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
             if (dcur == 0) {
               alive = false;
             } else {
-              uint32_t ux;
+              uint32_t ux, uy = 0u;
               if (kGwDiag && (A.diag & 2)) {
                 ux = ((uint32_t)s * 0x9E3779B1u) ^ ((uint32_t)g * 0x85EBCA6Bu) ^ ((uint32_t)t * 0xC2B2AE35u);
                 ux ^= ux >> 15;
                 ux *= 0x2C1B3C6Du;
               } else {
-                ux = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)t, 0u, A.k0, A.k1).x;
+                const gw_u4 u = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)t, 0u, A.k0, A.k1);
+                ux = u.x;
+                uy = u.y;
               }
-              const gw_ts_ent e = gw_ts_load(A.ent + ocur + gw_bounded(ux, (uint32_t)dcur));  // randNeighbor
+              const gw_ts_ent e = gw_ts_load(A.ent + ocur + gw_index(ux, uy, (uint32_t)dcur));  // randNeighbor
               path[t] = e.x;
               dpath[t] = e.d;
               dcur = e.d;

@@ -194,7 +194,7 @@ __global__ void __launch_bounds__(TD_BLOCK) k_topsim_levels(LvArgs A) {
         } else {
           const int g = W[j] >= 0 ? W[j] : walker_base + NW[j] + k;
           const gw_u4 u = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)(l + 1), call, A.k0, A.k1);
-          x = G.nbrs[G.offsets[v] + gw_bounded(u.x, (uint32_t)d)];
+          x = G.nbrs[G.offsets[v] + gw_index(u.x, u.y, (uint32_t)d)];
           nmass = m / (double)number;
           wid = g;
         }
@@ -331,7 +331,7 @@ __global__ void k_drw_walks(gw_dev_graph G, int sample, int step, uint32_t k0, u
         cur = -1;
       } else {
         const gw_u4 u = gw_philox((uint32_t)v, (uint32_t)i, (uint32_t)(t + 1), 0u, k0, k1);
-        cur = G.nbrs[G.offsets[cur] + gw_bounded(u.x, (uint32_t)d)];
+        cur = G.nbrs[G.offsets[cur] + gw_index(u.x, u.y, (uint32_t)d)];
       }
     }
     paths[w * step + t] = cur;  // -1 after a dead end (the Java loop stops there)

@@ -270,7 +270,7 @@ __global__ void __launch_bounds__(TM_BLOCK) k_topsim_m(TmArgs A) {
             const int d = G.deg[cur];
             if (d != 0) {
               const gw_u4 u = gw_philox((uint32_t)s, (uint32_t)w, (uint32_t)t, 0u, A.k0, A.k1);
-              cur = G.nbrs[G.offsets[cur] + gw_bounded(u.x, (uint32_t)d)];
+              cur = G.nbrs[G.offsets[cur] + gw_index(u.x, u.y, (uint32_t)d)];
               path[t] = cur;
               len = t;
               ++my_ext;
@@ -398,7 +398,7 @@ __global__ void __launch_bounds__(TM_BLOCK) k_topsim_m(TmArgs A) {
           } else {  // number random children (:153-164)
             const int g = Wl[j] >= 0 ? Wl[j] : walker_base + NW[j] + k;
             const gw_u4 u = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)(l + 1), 0u, A.k0, A.k1);
-            x = G.nbrs[G.offsets[v] + gw_bounded(u.x, (uint32_t)d)];
+            x = G.nbrs[G.offsets[v] + gw_index(u.x, u.y, (uint32_t)d)];
             nm = m / (double)number;
             wid = g;
           }

@@ -222,7 +222,7 @@ void or_walks_scale(int64_t n, const int64_t* off, const int32_t* nbrs, const do
       if (first_order || len == 1) {
         struct gw_u4 u = gw_philox(c0, c1, (uint32_t)len, 0u, k0, k1);
         ++tot_trials;
-        int64_t kk = gw_bounded(u.x, (uint32_t)d);
+        int64_t kk = gw_index(u.x, u.z, (uint32_t)d);
         if (w) kk = (gw_u01(u.y) < nq[b + kk]) ? kk : nJ[b + kk];
         slot = b + kk;
         next = nbrs[slot];
@@ -239,7 +239,9 @@ void or_walks_scale(int64_t n, const int64_t* off, const int32_t* nbrs, const do
             next = prev;
             break;
           }
-          int64_t kk = gw_bounded(u.x, (uint32_t)d);
+          /* low word of the 64-bit index draw: u.y unweighted, else one more Philox block */
+          const uint32_t ulo = w ? gw_philox(c0, c1, (uint32_t)len, (trial - 1u) | 0x80000000u, k0, k1).x : u.y;
+          int64_t kk = gw_index(u.x, ulo, (uint32_t)d);
           if (w) kk = (gw_u01(u.y) < nq[b + kk]) ? kk : nJ[b + kk];
           const int64_t s = b + kk;
           const int32_t x = nbrs[s];
@@ -491,7 +493,7 @@ static void topsim_one(const int64_t* off, const int32_t* nbrs, int variant, int
         int64_t k;
         if (rng == 0) {
           struct gw_u4 u = gw_philox((uint32_t)src, (uint32_t)i, (uint32_t)(pathLen + 1), 0u, k0, k1);
-          k = gw_bounded(u.x, (uint32_t)d);
+          k = gw_index(u.x, u.y, (uint32_t)d);
         } else {
           k = or_jrand_next_int(jr, (int32_t)d);
         }
@@ -591,7 +593,7 @@ static void topsim_one(const int64_t* off, const int32_t* nbrs, int variant, int
           int64_t k;
           if (rng == 0) {
             struct gw_u4 u = gw_philox((uint32_t)src, (uint32_t)wid, (uint32_t)(pathLen + 1), 0u, k0, k1);
-            k = gw_bounded(u.x, (uint32_t)d);
+            k = gw_index(u.x, u.y, (uint32_t)d);
           } else {
             k = or_jrand_next_int(jr, (int32_t)d);
           }
@@ -782,7 +784,7 @@ void or_topsim_levels(int64_t n, const int64_t* off, const int32_t* nbrs, int sa
               if (d == 0) break;
               int64_t wid = A.walker[pi] >= 0 ? A.walker[pi] : next_walker++;
               struct gw_u4 u = gw_philox((uint32_t)src, (uint32_t)wid, (uint32_t)(pathLen + 1), call, k0, k1);
-              int64_t k = gw_bounded(u.x, (uint32_t)d);
+              int64_t k = gw_index(u.x, u.y, (uint32_t)d);
               pq_reserve(&B, B.size + 1, L);
               int64_t c = B.size++;
               memcpy(B.cur + c * (L + 1), path, sizeof(int32_t) * (L + 1));
@@ -878,7 +880,7 @@ void or_double_random_walk(int64_t n, const int64_t* off, const int32_t* nbrs, i
           cur = -1;
         } else {
           struct gw_u4 u = gw_philox((uint32_t)v, (uint32_t)i, (uint32_t)(t + 1), 0u, k0, k1);
-          cur = nbrs[off[cur] + gw_bounded(u.x, (uint32_t)d)];
+          cur = nbrs[off[cur] + gw_index(u.x, u.y, (uint32_t)d)];
         }
         paths[(v * sample + i) * step + t] = cur;
         if (cur == -1) break;
@@ -985,9 +987,10 @@ int64_t or_simrank_round_rows(int64_t n, const int64_t* off, const int32_t* nbrs
 /* GW_N2V_BITSET restatement: the same 3-way exact mixture of the reference */
 /* get_alias_edge weights (node2vec.py:61-81; unweighted, undirected), but   */
 /* computing c and the common neighbours by explicit has_edge scans instead  */
-/* of precomputed bitsets.  Philox usage: step 1: u.x -> uniform neighbour;  */
-/* step >= 2: philox(w, step, 0).x -> component, .y -> first "other"        */
-/* candidate, philox(w, step, t).y -> retries t = 1, 2, ...                 */
+/* of precomputed bitsets.  Philox usage: step 1: (u.x:u.z) -> uniform       */
+/* neighbour (64-bit index draw); step >= 2: philox(w, step, 0).x ->        */
+/* component, (.y:.z) -> first "other" candidate, philox(w, step, t) (.y:.z) */
+/* -> retries t = 1, 2, ...                                                 */
 /* ------------------------------------------------------------------------ */
 void or_walks_bitset(int64_t n, const int64_t* off, const int32_t* nbrs, const int32_t* order, double p,
                      double q, uint64_t seed, int L, int64_t walk_begin, int64_t walk_count, int shuffle,
@@ -1017,7 +1020,7 @@ void or_walks_bitset(int64_t n, const int64_t* off, const int32_t* nbrs, const i
       struct gw_u4 u = gw_philox(c0, c1, (uint32_t)len, 0u, k0, k1);
       ++trial;
       if (len == 1) {
-        k = gw_bounded(u.x, (uint32_t)d);
+        k = gw_index(u.x, u.z, (uint32_t)d);
       } else {
         int64_t kp = -1, c = 0;
         for (int64_t j = 0; j < d; ++j) {
@@ -1044,7 +1047,7 @@ void or_walks_bitset(int64_t n, const int64_t* off, const int32_t* nbrs, const i
           }
         } else {
           for (;;) {
-            k = gw_bounded(u.y, (uint32_t)d);
+            k = gw_index(u.y, u.z, (uint32_t)d);
             int32_t x = nbrs[b + k];
             int bit = (x != prev) && find_slot(off, nbrs, prev, x) >= 0;
             if ((k != kp && !bit) || trial >= (1u << 24)) break;
