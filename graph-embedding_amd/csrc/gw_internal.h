@@ -150,6 +150,18 @@ struct gw_graph {
   std::string err;
 };
 
+// Scoped device selection for every C-ABI entry point that touches a device:
+// selects `dev` (the graph's device) for the call and restores the caller's
+// current device on return, so a call never changes the caller's (or torch's)
+// current device and a NULL stream launches on the graph's own device.
+struct gw_device_guard {
+  int prev = -1;
+  explicit gw_device_guard(int dev);
+  ~gw_device_guard();
+  gw_device_guard(const gw_device_guard&) = delete;
+  gw_device_guard& operator=(const gw_device_guard&) = delete;
+};
+
 // error helpers (gw_capi.cpp)
 int gw_fail(gw_graph* g, int code, const char* fmt, ...);
 void gw_set_tls_error(const std::string& s);

@@ -1104,6 +1104,7 @@ extern "C" int gw_topsim_host(gw_graph* g, int variant, int sample, int step, do
                               const int32_t* sources, int64_t nsrc, int topk, int32_t* out_ids,
                               double* out_scores, double* out_rows, int64_t* stats) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  gw_device_guard dg(g->device);  // restores the caller's current device on return
   if (g->device < 0) return gw_fail(g, GW_ERR_STATE, "graph is not on a device");
   if (nsrc < 0 || (nsrc > 0 && !sources) || (!out_rows && (!out_ids || !out_scores)) || topk < 0)
     return gw_fail(g, GW_ERR_INVALID, "bad arguments");

@@ -14,9 +14,17 @@
  *     (GW_OK == 0, negative = error); gw_last_error() gives the message.
  *   - no global mutable state: seeds, modes and device ordinals are explicit;
  *     one handle may be used from one thread at a time.
- *   - "_dev" pointers are device (HBM) pointers, "stream" is a hipStream_t
- *     (NULL = the default stream); such calls are asynchronous and launch-only
- *     (no allocation, no synchronisation) so they can be captured in a graph.
+ *   - every call that touches a device runs on the graph's device (or the
+ *     `device` argument) and restores the caller's current device on return.
+ *   - "_dev" pointers are device (HBM) pointers on the graph's device,
+ *     "stream" is a hipStream_t (NULL = the default stream).  gw_n2v_walks and
+ *     gw_simrank_naive (after its first call sized the workspace) are
+ *     asynchronous and launch-only (no allocation, no synchronisation), so they
+ *     can be captured in a HIP graph.  The TopSim calls (gw_topsim,
+ *     gw_topsim_dense, gw_topsim_m, gw_topsim_double, gw_topsim_dev,
+ *     gw_double_random_walk) synchronise the stream before returning (they
+ *     read the kernels' capacity flag to fail loudly) and size their
+ *     workspace on first use (gw_topsim_prepare does it ahead of time).
  *   - all other pointers are host pointers, caller-allocated; size them with
  *     gw_graph_info() / the documented formulas.
  *   - vertex ids crossing the boundary are dense ids in [0, n) unless a

@@ -473,3 +473,27 @@ def test_walk_shapes_edge_cases(gw, oracle, mode, p, q):
                 ref, rl, _ = oracle.walks_scale(dict(csr, weights=None), p, q, 13, L, begin, count, nthreads=4)
             np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"count={count} L={L}")
             np.testing.assert_array_equal(lens.cpu().numpy(), rl)
+
+
+def test_calls_run_on_the_graph_device_and_keep_the_callers(gw, oracle):
+    """Every C-ABI call runs on the graph's device and restores the caller's
+    current device: the graph lives on the LAST visible device while
+    the caller's current device is 0, the walk launch uses the NULL stream, and
+    the walks still equal the oracle (on a one-GPU box both are device 0)."""
+    import torch
+    from gwamd import _lib as C
+    dev = torch.cuda.device_count() - 1
+    torch.cuda.set_device(0)
+    G = gw.GWGraph.from_edgelist(os.path.join(DATA, "karate.edgelist"), " ", "nx").to_device(dev)
+    assert torch.cuda.current_device() == 0
+    C.check(C.lib().gw_n2v_prepare(G.handle, 0.25, 4.0, C.N2V_REJECTION), G.handle)
+    assert torch.cuda.current_device() == 0
+    nw, L = 200, 20
+    out = torch.empty((nw, L), dtype=torch.int32, device=f"cuda:{dev}")
+    C.check(C.lib().gw_n2v_walks(G.handle, L, 3, 0, nw, 1, C.ptr(out), None, None, None), G.handle)
+    assert torch.cuda.current_device() == 0
+    torch.cuda.synchronize(dev)
+    ref, _, _ = oracle.walks_scale(dict(G.export_csr(), weights=None), 0.25, 4.0, 3, L, 0, nw)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    G.free()
+    assert torch.cuda.current_device() == 0
