@@ -26,6 +26,7 @@ int gw_write_sim_dense_impl(const char* path, const double* rows, const int32_t*
 int gw_write_sim_topk_impl(const char* path, const int32_t* ids, const double* scores,
                            const int32_t* row_ids, int64_t nrows, int topk,
                            const std::string& sep, int decimals, std::string* err);
+void gw_java_double_to_string(double v, std::string* out);
 int gw_write_sim_cachemap_impl(const char* path, const int32_t* keys, const float* vals, const int32_t* sizes,
                                const int32_t* row_ids, int64_t nrows, int capacity, int topk,
                                const std::string& sep, std::string* err);
@@ -447,4 +448,14 @@ int gw_write_sim_text_cachemap(const char* path, const int32_t* keys, const floa
   return GW_OK;
 }
 
+int gw_format_java_double(double v, char* buf, int64_t buflen) {
+  std::string s;
+  gw_java_double_to_string(v, &s);
+  if (!buf || buflen < (int64_t)s.size() + 1) return gw_fail(nullptr, GW_ERR_RANGE, "buffer too small (%lld B needed)",
+                                                             (long long)s.size() + 1);
+  memcpy(buf, s.c_str(), s.size() + 1);
+  return GW_OK;
+}
+
 }  // extern "C"
+

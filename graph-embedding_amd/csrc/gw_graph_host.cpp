@@ -633,6 +633,52 @@ struct JavaPQ {
   }
 };
 
+// Double.toString / string concatenation of a double (Java): shortest
+// round-trip digits; plain notation with at least one fraction digit for
+// 1e-3 <= |v| < 1e7, else computerized scientific "d.dddE[-]n" (JLS
+// Double.toString).  Eval.precision writes its scores this way (Eval.java:118).
+void gw_java_double_to_string(double v, std::string* out) {
+  if (std::isnan(v)) {
+    *out += "NaN";
+    return;
+  }
+  if (std::isinf(v)) {
+    *out += v > 0 ? "Infinity" : "-Infinity";
+    return;
+  }
+  if (v == 0.0) {
+    *out += std::signbit(v) ? "-0.0" : "0.0";
+    return;
+  }
+  char buf[64];
+  auto r = std::to_chars(buf, buf + sizeof buf, v, std::chars_format::scientific);
+  std::string s(buf, r.ptr);  // [-]d[.ddd]e[+-]xx  (shortest round-trip)
+  size_t i = 0;
+  if (s[0] == '-') {
+    *out += '-';
+    i = 1;
+  }
+  const size_t epos = s.find('e');
+  std::string digits;
+  for (size_t k = i; k < epos; ++k)
+    if (s[k] != '.') digits.push_back(s[k]);
+  const int e = atoi(s.c_str() + epos + 1);  // value = d1.d2d3... * 10^e
+  const double a = std::fabs(v);
+  if (a >= 1e-3 && a < 1e7) {
+    if (e >= 0) {
+      std::string ip = digits.substr(0, std::min(digits.size(), (size_t)e + 1));
+      if ((int)ip.size() < e + 1) ip += std::string((size_t)e + 1 - ip.size(), '0');
+      std::string fp = digits.size() > (size_t)e + 1 ? digits.substr((size_t)e + 1) : std::string("0");
+      *out += ip + "." + fp;
+    } else {
+      *out += "0." + std::string((size_t)(-e - 1), '0') + digits;
+    }
+  } else {
+    *out += digits.substr(0, 1) + "." + (digits.size() > 1 ? digits.substr(1) : std::string("0")) + "E" +
+            std::to_string(e);
+  }
+}
+
 // String.format("%.Nf") in Java 8: FloatingDecimal digits, HALF_UP rounding.
 void gw_java_format_fixed(double v, int decimals, std::string* out) {
   if (std::isnan(v)) {

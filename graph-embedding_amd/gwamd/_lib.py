@@ -124,6 +124,7 @@ SIGNATURES = {
     "gw_double_sim_host": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           D, U64, P, P]),
     "gw_select_fixed_max_pq": (ctypes.c_int, [P, I64, I64, ctypes.c_int, D, P]),
+    "gw_format_java_double": (ctypes.c_int, [D, ctypes.c_char_p, I64]),
     "gw_simrank_naive": (ctypes.c_int, [P, D, ctypes.c_int, P, P]),
     "gw_simrank_naive_host": (ctypes.c_int, [P, D, ctypes.c_int, P]),
     "gw_write_walks_text": (ctypes.c_int, [P, CP, P, P, I64, ctypes.c_int]),

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <fstream>
 #include <iostream>
+#include <limits>
 #include <set>
 #include <sstream>
 
@@ -198,6 +199,13 @@ static std::vector<std::string> split(const std::string& s, const std::string& s
   return out;
 }
 
+// Java's Double.toString (libgraphwalk gw_format_java_double)
+static std::string java_double(double v) {
+  char buf[64];
+  if (gw_format_java_double(v, buf, sizeof buf) != GW_OK) return "NaN";
+  return buf;
+}
+
 std::string Eval::precision(const std::string& path1, const std::string& path2, const std::string& prePath, int K) {
   (void)K;  // the reference uses MyConfiguration.TOPK (Eval.java:112)
   std::ifstream in1(path1), in2(path2);
@@ -205,7 +213,7 @@ std::string Eval::precision(const std::string& path1, const std::string& path2, 
   std::ofstream out(prePath, std::ios::binary);
   const std::string& sep = conf::MyConfiguration::SEPARATOR;
   const std::string& kv = conf::MyConfiguration::SEPARATOR_KV;
-  double sum = 0, mn = 1e300;
+  double sum = 0, mn = std::numeric_limits<double>::max();  // Double.MAX_VALUE (Eval.java:89)
   long total = 0;
   std::string l1, l2;
   while (std::getline(in1, l1)) {
@@ -236,16 +244,13 @@ std::string Eval::precision(const std::string& path1, const std::string& path2, 
       pre = 1.0 * inter / realK;
     }
     sum += pre;
-    std::ostringstream os;
-    os << t1[0] << sep << pre << "\r\n";
-    out << os.str();
+    out << t1[0] << sep << java_double(pre) << "\r\n";  // Java "" + double (Eval.java:118)
     ++total;
     mn = std::min(mn, pre);
   }
-  std::cout << "total nodes:" << total << "\tavg precision: " << sum / std::max<long>(total, 1)
-            << "\tmin pre: " << mn << std::endl;
-  std::ostringstream r;
-  r << sum / std::max<long>(total, 1);
-  return r.str();
+  const double avg = sum / (double)total;  // NaN for an empty gold file, as in Java (0.0 / 0)
+  std::cout << "total nodes:" << total << "\tavg precision: " << java_double(avg)
+            << "\tmin pre: " << java_double(mn) << std::endl;  // min stays Double.MAX_VALUE when empty
+  return java_double(avg);
 }
 }  // namespace utils

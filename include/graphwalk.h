@@ -293,6 +293,11 @@ int gw_double_sim_host(gw_graph* g, int kind, int sample, int step, int topK,
  * sortedElement() -> out_ids[r*k + i] (-1 padded).  Host code.             */
 int gw_select_fixed_max_pq(const double* rows, int64_t nrows, int64_t n, int k,
                            double min_score, int32_t* out_ids);
+/* Java's Double.toString of v (string concatenation "" + v), as
+ * Eval.precision writes its scores (Eval.java:118, :128): shortest round-trip
+ * digits, plain for 1e-3 <= |v| < 1e7 (at least one fraction digit), else
+ * "d.dddE[-]n".  NUL-terminated into buf[buflen]; GW_ERR_RANGE if too small. */
+int gw_format_java_double(double v, char* buf, int64_t buflen);
 
 /* ---- naive SimRank (TopSim ground truth) ------------------------------------ */
 /* Replaces new SimRank(g).compute() + getResult() (SimRank.java:21-57, 79):

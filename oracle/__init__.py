@@ -398,6 +398,32 @@ def read_graph_nx_semantics(path, delimiter, weighted, directed):
             np.array(nbrs, np.int32), np.array(wts, np.float64))
 
 
+def java_double_to_string(v):
+    """Java Double.toString(v) / "" + v (JLS): shortest round-trip digits
+    (Python repr's), plain with >= 1 fraction digit for 1e-3 <= |v| < 1e7,
+    else "d.dddE[-]n".  (JDK <= 18 printed a few values, e.g. subnormals, with
+    extra digits; not emulated.)"""
+    import math
+    v = float(v)
+    if v != v:
+        return "NaN"
+    if math.isinf(v):
+        return "Infinity" if v > 0 else "-Infinity"
+    if v == 0.0:
+        return "-0.0" if math.copysign(1.0, v) < 0 else "0.0"
+    sign, digits, exp = decimal.Decimal(repr(v)).normalize().as_tuple()
+    ds = "".join(map(str, digits))
+    e = len(ds) - 1 + exp
+    if 1e-3 <= abs(v) < 1e7:
+        if e >= 0:
+            body = ds[:e + 1].ljust(e + 1, "0") + "." + (ds[e + 1:] or "0")
+        else:
+            body = "0." + "0" * (-e - 1) + ds
+    else:
+        body = ds[0] + "." + (ds[1:] or "0") + "E" + str(e)
+    return ("-" if sign else "") + body
+
+
 def java_format_fixed(v, decimals=6):
     """Java 8 String.format("%.Nf", v): shortest repr digits, HALF_UP."""
     d = decimal.Decimal(repr(float(v)))

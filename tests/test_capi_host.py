@@ -284,3 +284,44 @@ def test_release_library_has_no_diagnostic_knobs(gw):
     with open(_lib.LIB_PATH, "rb") as f:
         blob = f.read()
     assert b"GW_DIAG" not in blob
+
+
+def test_java_double_to_string_matches_java(gw, oracle):
+    """gw_format_java_double == Java's Double.toString (Eval.java:118 writes
+    precision values this way) on known Java outputs and random doubles."""
+    import ctypes
+    from gwamd import _lib as C
+
+    def fmt(v):
+        buf = ctypes.create_string_buffer(64)
+        C.check(C.lib().gw_format_java_double(float(v), buf, 64))
+        return buf.value.decode()
+    known = [(1.0, "1.0"), (0.0, "0.0"), (-0.0, "-0.0")] + list({0.5: "0.5", 0.001: "0.001", 1e-4: "1.0E-4",
+             1e7: "1.0E7", 9999999.0: "9999999.0", 123456789.0: "1.23456789E8", 0.1 + 0.2: "0.30000000000000004",
+             2 / 3: "0.6666666666666666", -2.5: "-2.5", 100.0: "100.0", 0.05: "0.05", 1234.5678: "1234.5678",
+             -3.2e-5: "-3.2E-5", 1.5e300: "1.5E300", float("nan"): "NaN", float("inf"): "Infinity"}.items())
+    for v, s in known:
+        assert fmt(v) == s, (v, fmt(v), s)
+        assert oracle.java_double_to_string(v) == s, (v, s)
+    rng = np.random.default_rng(5)
+    for v in np.concatenate([rng.random(300), rng.random(200) * 10.0 ** rng.integers(-8, 12, 200),
+                             -rng.random(50) * 1e3, np.arange(0, 21) / 20.0]):
+        assert fmt(v) == oracle.java_double_to_string(v), v
+    buf = ctypes.create_string_buffer(3)
+    assert C.lib().gw_format_java_double(0.123, buf, 3) == C.GW_ERR_RANGE
+
+
+def test_read_simrank_reads_topk_writer_output(gw, tmp_path):
+    """gwamd.io.read_simrank (DeepSim/src/main.py:83-107) on a .sim.txt that
+    gw_write_sim_text_topk wrote: rows in order, ids in score order, values
+    <= 1e-8 (printed 0.000000) dropped."""
+    from gwamd import _lib as C
+    from gwamd.io import read_simrank
+    ids = np.array([[4, 1, 2], [0, 3, 2], [1, 0, 4]], np.int32)
+    sc = np.array([[0.75, 0.125, 0.0], [3.5, 1e-9, 0.0], [2.0000005, 0.0, 0.0]], np.float64)
+    rid = np.array([0, 1, 2], np.int32)
+    path = str(tmp_path / "topk")
+    C.check(C.lib().gw_write_sim_text_topk(path.encode(), C.ptr(ids), C.ptr(sc), C.ptr(rid), 3, 3, b",", 6))
+    got = read_simrank(path + ".sim.txt")
+    assert [[i for i, _ in row] for row in got] == [["4", "1"], ["0"], ["1"]]
+    assert [[float(v) for _, v in row] for row in got] == [[0.75, 0.125], [3.5], [2.000001]]
