@@ -194,7 +194,8 @@ int gw_build_java_multi(gw_graph* g, int64_t m, const int64_t* src,
 static bool is_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f'; }
 
 // Python int(): optional surrounding whitespace, sign, digits (underscores
-// between digits are accepted by Python; accepted here too).
+// between digits are accepted by Python; accepted here too).  Labels must fit
+// int64 (Python's ints are unbounded: larger labels are refused as a parse error).
 static bool parse_py_int(const char* b, const char* e, int64_t* out) {
   while (b < e && is_space(*b)) ++b;
   while (e > b && is_space(e[-1])) --e;
@@ -209,6 +210,7 @@ static bool parse_py_int(const char* b, const char* e, int64_t* out) {
   bool last_digit = false;
   for (const char* p = b; p < e; ++p) {
     if (*p >= '0' && *p <= '9') {
+      if (v > (INT64_MAX - (*p - '0')) / 10) return false;  // beyond int64
       v = v * 10 + (*p - '0');
       last_digit = true;
     } else if (*p == '_' && last_digit && p + 1 < e && p[1] >= '0' && p[1] <= '9') {

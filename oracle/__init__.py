@@ -23,7 +23,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "liboracle.so")
+LIB = os.environ.get("GW_ORACLE_LIB", os.path.join(HERE, "liboracle.so"))  # (sanitizer runs: tools/sanitize.sh)
 _lib = None
 
 
@@ -34,7 +34,8 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, "oracle.c")):
+        if LIB == os.path.join(HERE, "liboracle.so") and (
+                not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, "oracle.c"))):
             build()
         L = ctypes.CDLL(LIB)
         v, i64, i32, d, u64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_double, ctypes.c_uint64

@@ -325,3 +325,46 @@ def test_read_simrank_reads_topk_writer_output(gw, tmp_path):
     got = read_simrank(path + ".sim.txt")
     assert [[i for i, _ in row] for row in got] == [["4", "1"], ["0"], ["1"]]
     assert [[float(v) for _, v in row] for row in got] == [[0.75, 0.125], [3.5], [2.000001]]
+
+
+MALFORMED = [
+    b"", b"\n\n\n", b"# only a comment\n", b"1", b"1 ", b"1 2 3 4 5\n", b"a b\n", b"1 b\n", b"1 2\n3",
+    b"99999999999999999999999 1\n", b"-1 2\n", b"1 -2\n", b"1\x002\n", b"\xff\xfe 1\n", b"1 2 nan\n", b"1 2 inf\n",
+    b"1 2 1e999\n", b"1 2 -0.5\n", b"1\t2\n", b"1  2\n", b"\r\r\r", b"1 2\r3 4\r", b" 1 2\n", b"1 2 \n",
+    b"1" * 100000 + b" 2\n", (b"1 2\n" * 50000)[:-3],
+]
+
+
+@pytest.mark.parametrize("blob", MALFORMED, ids=[str(i) for i in range(len(MALFORMED))])
+@pytest.mark.parametrize("sem", ["nx", "java"])
+def test_loaders_survive_malformed_input(gw, tmp_path, blob, sem):
+    """Malformed, truncated and oversized edge lists (Graph.java:38-39 and
+    networkx read_edgelist error cases): the loaders either build a graph or
+    raise a library error — never crash (tools/sanitize.sh runs this under
+    ASan/UBSan)."""
+    from gwamd import _lib as C
+    p = tmp_path / "m.txt"
+    p.write_bytes(blob)
+    for weighted in (False, True):
+        try:
+            g = gw.GWGraph.from_edgelist(str(p), " ", sem, False, weighted, vcount=5 if sem == "java" else -1)
+        except (C.GraphWalkError, ValueError, IndexError, KeyError, OSError, ZeroDivisionError):
+            continue
+        csr = g.export_csr()
+        assert csr["offsets"][-1] == len(csr["nbrs"]) and np.all(np.diff(csr["offsets"]) >= 0)
+        if len(csr["nbrs"]):
+            assert csr["nbrs"].min() >= 0 and csr["nbrs"].max() < len(csr["offsets"]) - 1
+        g.free()
+
+
+def test_generators_and_csr_reject_bad_sizes(gw):
+    from gwamd import _lib as C
+    for scale, ef in ((-1, 16), (0, 16), (63, 16), (10, -3), (10, 0)):
+        try:
+            gw.GWGraph.rmat(scale, ef).free()
+        except (C.GraphWalkError, ValueError, MemoryError):
+            pass
+    with pytest.raises(Exception):
+        gw.GWGraph.from_csr(np.array([0, 3, 2], np.int64), np.array([1, 0, 1], np.int32))  # offsets decrease
+    with pytest.raises(Exception):
+        gw.GWGraph.from_csr(np.array([0, 1, 2], np.int64), np.array([1, 7], np.int32))  # neighbour id >= n
