@@ -88,6 +88,15 @@ def build(force=False, verbose=False, diag=False):
               "-Wl,--no-undefined"], verbose)
     if diag:
         return OUT
+    # JNI shim for a Java host (north_star): only where a JDK provides jni.h
+    jh = os.environ.get("JAVA_HOME")
+    if jh and os.path.exists(os.path.join(jh, "include", "jni.h")):
+        jni_src = os.path.join(HERE, "jni", "graphwalk_jni.c")
+        jni_out = os.path.join(HERE, "gwamd", "libgraphwalk_jni.so")
+        if force or _newer(jni_out, [jni_src, OUT, os.path.join(ROOT, "include", "graphwalk.h")]):
+            _run(["gcc", "-O2", "-shared", "-fPIC", "-Wall", f"-I{jh}/include", f"-I{jh}/include/linux",
+                  f"-I{os.path.join(ROOT, 'include')}", jni_src, f"-L{os.path.dirname(OUT)}", "-lgraphwalk",
+                  "-Wl,-rpath,$ORIGIN", "-o", jni_out], verbose)
     # C++ host mirror of the Java TopSim API + the benchmark driver binary
     host = os.path.join(HERE, "host")
     bindir = os.path.join(HERE, "bin")

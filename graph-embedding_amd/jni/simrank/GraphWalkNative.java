@@ -1,0 +1,43 @@
+package simrank;
+
+/**
+ * Native bindings of libgraphwalk (include/graphwalk.h) through
+ * graph-embedding_amd/jni/graphwalk_jni.c.
+ *
+ * UNTESTED HERE: the build image has no JDK; build.py compiles the shim only
+ * when $JAVA_HOME/include/jni.h exists.  Load order: libgraphwalk.so, then
+ * libgraphwalk_jni.so (java.library.path = graph-embedding_amd/gwamd).
+ */
+public final class GraphWalkNative {
+    static {
+        System.loadLibrary("graphwalk");
+        System.loadLibrary("graphwalk_jni");
+    }
+
+    /** include/graphwalk.h GW_TOPSIM_* variants. */
+    public static final int TOPSIM_SINGLE_SAMPLE = 0, TOPSIM_ENUMERATE = 1, TOPSIM_SINGLE_RW = 2;
+
+    private GraphWalkNative() {}
+
+    /** structures.Graph(path, V) (Graph.java:28-42) with the given separator, on GPU `device`. */
+    public static native long loadGraph(String path, String separator, int V, int device) throws java.io.IOException;
+
+    public static native void freeGraph(long g);
+
+    public static native int vertexCount(long g);
+
+    /** TopSim rows for `sources` as dense V-length rows (getResult() of those sources). */
+    public static native void topsimDense(long g, int variant, int sample, int step, double C, long seed,
+                                          int[] sources, double[][] simOut, long[] stats);
+
+    /** TopSim top-k rows for any V: ids / scores of length sources.length * k. */
+    public static native void topsimTopK(long g, int variant, int sample, int step, double C, long seed,
+                                         int[] sources, int k, int[] idsOut, double[] scoresOut, long[] stats);
+
+    /** simrank.SimRank(g).compute() + getResult(): V*V row-major, diagonal 0 (SimRank.java:36-81). */
+    public static native void simrankNaive(long g, double C, int step, double[] simOut);
+
+    /** utils.Print.printByOrder files (Print.java:25-53) from top-k rows. */
+    public static native void writeTopK(String path, int[] ids, double[] scores, int[] rowIds, int k,
+                                        String separator);
+}

@@ -1,0 +1,55 @@
+package simrank;
+
+import conf.MyConfiguration;
+
+/**
+ * Drop-in for simrank.TopSim_singleSample (TopSim_singleSample.java:35-58) on
+ * the GPU: same constructor arguments and compute() / getResult(), plus topK()
+ * for graphs whose dense V x V result does not fit.  Scores are SAMPLE x
+ * SimRank like the reference's (not divided by SAMPLE).  Random draws are
+ * Philox-keyed by (seed, source, walker, level) instead of the reference's
+ * unseeded static java.util.Random (Graph.java:17).
+ *
+ * UNTESTED HERE (no JDK in the build image); the C++ port of the same driver
+ * (graph-embedding_amd/host/) runs in the GPU tests.
+ */
+public class TopSim_singleSampleNative {
+    private final long g;
+    private final int V, sample, step;
+    private final long seed;
+    private double[][] sim;
+
+    public TopSim_singleSampleNative(String path, int V, int sample, int step, long seed, int device)
+            throws java.io.IOException {
+        this.g = GraphWalkNative.loadGraph(path, MyConfiguration.SEPARATOR, V, device);
+        this.V = V;
+        this.sample = sample;
+        this.step = step;
+        this.seed = seed;
+    }
+
+    /** every source i in 0..V-1, dense rows (TopSim_singleSample.compute(), :47-54). */
+    public void compute() {
+        int[] all = new int[V];
+        for (int i = 0; i < V; i++) all[i] = i;
+        sim = new double[V][V];
+        GraphWalkNative.topsimDense(g, GraphWalkNative.TOPSIM_SINGLE_SAMPLE, sample, step, MyConfiguration.C, seed,
+                                    all, sim, null);
+    }
+
+    public double[][] getResult() {
+        return sim;
+    }
+
+    /** top-k rows of `sources` (ids -1 padded): the path for graphs where V x V doubles do not fit. */
+    public int[] topK(int[] sources, int k, double[] scoresOut) {
+        int[] ids = new int[sources.length * k];
+        GraphWalkNative.topsimTopK(g, GraphWalkNative.TOPSIM_SINGLE_SAMPLE, sample, step, MyConfiguration.C, seed,
+                                   sources, k, ids, scoresOut, null);
+        return ids;
+    }
+
+    public void close() {
+        GraphWalkNative.freeGraph(g);
+    }
+}

@@ -368,3 +368,24 @@ def test_generators_and_csr_reject_bad_sizes(gw):
         gw.GWGraph.from_csr(np.array([0, 3, 2], np.int64), np.array([1, 0, 1], np.int32))  # offsets decrease
     with pytest.raises(Exception):
         gw.GWGraph.from_csr(np.array([0, 1, 2], np.int64), np.array([1, 7], np.int32))  # neighbour id >= n
+
+
+def test_jni_shim_calls_only_exported_abi(gw):
+    """graph-embedding_amd/jni/graphwalk_jni.c (built only where a JDK exists,
+    untested here): every gw_* function it calls is declared in
+    include/graphwalk.h and exported by libgraphwalk.so, and every native
+    method of simrank.GraphWalkNative has its Java_simrank_GraphWalkNative_* C
+    definition."""
+    from gwamd import _lib as C
+    jni = open(os.path.join(ROOT, "graph-embedding_amd", "jni", "graphwalk_jni.c")).read()
+    hdr = open(os.path.join(ROOT, "include", "graphwalk.h")).read()
+    called = set(re.findall(r"\b(gw_[a-z0-9_]+)\(", jni)) - {"gw_graph_info_t"}
+    declared = set(re.findall(r"\bint (gw_[a-z0-9_]+)\(", hdr)) | set(re.findall(r"\b(gw_last_error)\(", hdr))
+    assert called and called <= declared, called - declared
+    lib = C.lib()
+    for f in called:
+        getattr(lib, f)
+    java = open(os.path.join(ROOT, "graph-embedding_amd", "jni", "simrank", "GraphWalkNative.java")).read()
+    natives = set(re.findall(r"public static native \w+ (\w+)\(", java))
+    defined = set(re.findall(r"Java_simrank_GraphWalkNative_(\w+)\(", jni))
+    assert natives and natives == defined, (natives, defined)
