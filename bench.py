@@ -170,17 +170,35 @@ def lib_digest():
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
-def load_prof(tag, units=None, key="walk_steps_per_launch"):
-    """PMC summary entry measured on this exact library build (and workload)."""
+def load_prof(tag, units=None):
+    """PMC summary entry (tools/pmc_summary.py) measured on this exact library
+    build and workload size, else None."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(p) as f:
             e = json.load(f).get(tag)
-        if e and e.get("lib_sha256") == lib_digest() and (units is None or e.get(key) == units):
+        if e and e.get("lib_sha256") == lib_digest() and (units is None or e.get("units_per_launch") == units):
             return e
     except Exception:
         pass
     return None
+
+
+def grid_threads(count, block=256):
+    return (count + block - 1) // block * block
+
+
+def line_roofline(prof, kernel_s, table_bytes, block=64):
+    """Fabric read requests per second of the profiled launch against the
+    calibrated random-block rate for a table of that size (one request per
+    random 32-128 B block, profiles/calib_r02.json)."""
+    peak, table_mb = calib_rate(table_bytes, block)
+    r = {"calibrated_peak_lines_per_s": peak, "calib_table_mb": table_mb, "calib_file": os.path.relpath(CALIB_FILE, ROOT)}
+    if prof and prof.get("fabric_read_requests_per_launch"):
+        lr = prof["fabric_read_requests_per_launch"] / kernel_s
+        r.update({"achieved_lines_per_s": lr, "frac": lr / peak,
+                  "lines_per_unit": prof["fabric_read_requests_per_launch"] / max(prof["units_per_launch"], 1)})
+    return r
 
 
 def cores_used():
@@ -479,13 +497,12 @@ def walk_headline(R, args):
     tag = f"n2v_rmat{args.scale}_ef{args.edge_factor}_p{args.p}_q{args.q}_L{L}_r{args.num_walks}_{mode}"
     prof = load_prof(tag, launch_steps)
     traffic = prof["hbm_bytes_per_launch"] if prof else None
-    peak_lines, table_mb = calib_rate(sampler_bytes if mode == "bitset" else max(sampler_bytes, 16 * nnz))
-    line_rate = {"calibrated_peak_lines_per_s": peak_lines, "calib_table_mb": table_mb,
-                 "calib_file": os.path.relpath(CALIB_FILE, ROOT)}
-    if prof and prof.get("fabric_read_requests_per_launch"):
-        lr = prof["fabric_read_requests_per_launch"] / (k_avg_ms * 1e-3)
-        line_rate.update({"achieved_lines_per_s": lr, "frac": lr / peak_lines,
-                          "lines_per_step": prof["fabric_read_requests_per_launch"] / max(launch_steps, 1)})
+    table = sampler_bytes if mode == "bitset" else max(sampler_bytes, 16 * nnz)
+    line_rate = line_roofline(prof, k_avg_ms * 1e-3, table)
+    # structural ceiling of the 36 B/step metric: every step reads at least one
+    # random block (one fabric request), so at the calibrated request rate
+    line_rate["ceiling_frac_at_one_request_per_step"] = \
+        BYTES_PER_STEP * line_rate["calibrated_peak_lines_per_s"] / (HBM_PEAK_GBS * 1e9)
 
     # ---- parity spot check (cheap): every step of a sample follows an edge ----
     if rank == 0:
@@ -510,6 +527,7 @@ def walk_headline(R, args):
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                         "traffic_note": (prof or {}).get("note"),
+                        "pmc_tag": tag, "pmc_match": {"kernel": kname, "grid": grid_threads(B)},
                         "kernel": kname, "kernel_ms": k_avg_ms,
                         "bytes_per_unit": BYTES_PER_STEP, "units_per_launch": launch_steps,
                         "lib_sha256": lib_digest(), "random_line_roofline": line_rate}}
@@ -574,6 +592,11 @@ def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejectio
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu_b = cpu_baseline_walks(BG.export_csr(), wp, wq, args.seed, L, 0, 10.0, max_walks=2_000_000)
     del bout
+    kname = "k_walk_bitset" if bmode == "bitset" else "k_walk_scale"
+    tag = f"n2v_rmat{scale}_ef{ef}_p{wp}_q{wq}_L{L}_r{walks_per_node}_{bmode}"
+    prof = load_prof(tag, local_steps)
+    sbytes = BG.info().sampler_bytes
+    line = line_roofline(prof, kms * 1e-3, sbytes if bmode == "bitset" else max(sbytes, 16 * bi.nnz))
     return {"metric": f"walk-steps/sec (node2vec, {what})", "value": bsteps / sec, "unit": "walk-steps/s",
             "n_ranks": world, "scaling": "weak",
             "config": {"workload": f"node2vec p={wp} q={wq} on Graph500 R-MAT scale-{scale} ef {ef} "
@@ -583,7 +606,10 @@ def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejectio
             "roofline": {"bound": "hbm", "achieved": BYTES_PER_STEP * local_steps / (kms * 1e-3) / 1e9,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": BYTES_PER_STEP * local_steps / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "traffic": None, "kernel": "k_walk_bitset" if bmode == "bitset" else "k_walk_scale"},
+                         "traffic": prof["hbm_bytes_per_launch"] if prof else None, "kernel": kname,
+                         "units_per_launch": local_steps, "pmc_tag": tag,
+                         "pmc_match": {"kernel": kname, "grid": grid_threads(nb)},
+                         "random_line_roofline": line},
             "host_build_s": build_s, "prepare_s": bprep, "sampler_tables_gb": BG.info().sampler_bytes / 1e9,
             "cpu_baseline": cpu_b}
 
@@ -593,25 +619,30 @@ TOPSIM_GRAPHS = {"blog": ("blog.txt", 10313, ",", "lshrank blog, V=10313, 333,98
                  "moreno": ("moreno_crime_crime.txt", 1380, "\t", "lshrank moreno, V=1380, 1,476 edges")}
 
 
-def topsim_roofline(ext, upd, kt, tag, nsrc):
+def topsim_roofline(ext, upd, kt, tag, nsrc, nnz, step):
     """52 B per path extension + 24 B per pair-update / kernel time.
-    When the PMC traffic of this library build shows fewer HBM bytes than the
-    algorithmic count (cache-resident slot table and level records, LDS
-    accumulator), the bound is relabelled L2 and priced against 34.5 TB/s."""
+    The denominator follows where the data lives: the slot table (16 B per
+    adjacency entry) and the level records of lshrank graphs stay in the 256 MB
+    Infinity Cache (MI355X_MICROARCH.md §Infinity Cache), so their bound is the
+    calibrated random-block rate of a cache-resident table x 128 B, not 8 TB/s;
+    P10M's 3.2 GB slot table is HBM.  traffic = HBM-side bytes from the PMC
+    passes of this library build (2 x FETCH_SIZE + WRITE_SIZE, as
+    tools/pmc_summary.py documents), or null."""
     alg = TOPSIM_B_EXT * ext + TOPSIM_B_UPD * upd
-    prof = load_prof(tag, nsrc, key="sources")
-    traffic = prof["hbm_bytes_per_launch"] if prof else None
+    prof = load_prof(tag, nsrc)
     achieved = alg / kt / 1e9
-    if traffic is not None and traffic >= alg:
-        bound, peak = "hbm", HBM_PEAK_GBS
-    elif traffic is not None:
-        bound, peak = "l2", L2_PEAK_GBS
+    table = 16 * nnz
+    rate, table_mb = calib_rate(table, 128)
+    if table <= 200 << 20:
+        bound, peak = "infinity-cache (random 128 B blocks)", rate * 128 / 1e9
     else:
-        bound, peak = "unmeasured (no PMC pass for this library build)", None
-    return {"bound": bound, "achieved": achieved, "peak": peak, "unit": "GB/s",
-            "frac": achieved / peak if peak else None, "traffic": traffic,
-            "traffic_GBps": traffic / kt / 1e9 if traffic else None,
-            "algorithmic_bytes": alg, "kernel": "k_topsim", "kernel_ms": kt * 1e3}
+        bound, peak = "hbm", HBM_PEAK_GBS
+    return {"bound": bound, "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
+            "traffic": prof["hbm_bytes_per_launch"] if prof else None,
+            "traffic_GBps": prof["hbm_bytes_per_launch"] / kt / 1e9 if prof else None,
+            "algorithmic_bytes": alg, "slot_table_bytes": table, "kernel": "k_topsim", "kernel_ms": kt * 1e3,
+            "units_per_launch": nsrc, "pmc_tag": tag, "pmc_match": {"kernel": f"k_topsim(_2wg)?<{step},", "grid": None},
+            "random_line_roofline": line_roofline(prof, kt, table, 128)}
 
 
 def run_topsim(R, args, name):
@@ -691,7 +722,7 @@ def run_topsim(R, args, name):
         "config": {"workload": f"TopSim_singleSample on {name} ({desc}, Java multigraph)",
                    "step": step, "sample": sample, "C": 0.6, "topk": K},
         "pair_updates": upd, "path_extensions": ext, "seconds": tel, "cpu_baseline": cpu_ts,
-        "roofline": topsim_roofline(ext_l, upd_l, kms * 1e-3, tag, nloc),
+        "roofline": topsim_roofline(ext_l, upd_l, kms * 1e-3, tag, nloc, int(offs[-1]), step),
     }
 
 

@@ -1,70 +1,105 @@
-"""Summarise rocprofv3 PMC passes into profiles/pmc_summary.json.
+"""Summarise rocprofv3 PMC passes of the bench into profiles/pmc_summary.json.
 
-    python tools/pmc_summary.py TAG FETCH_CSV WRITE_CSV BENCH_JSON
+    python tools/pmc_summary.py FETCH_DIR WRITE_DIR RDREQ_DIR BENCH_JSON
 
-HBM traffic per launch = (FETCH_SIZE + WRITE_SIZE) * 1024 bytes, averaged
-over the dispatches of the kernel (MI355X_MICROARCH.md §HBM: both counters
-are in KiB, read from TCC_EA0 memory-side requests; Infinity-Cache hits are
-counted).  The gfx950 x2 correction for FETCH_SIZE applies to wide (16 B per
-lane) coalesced streaming reads only; the walk kernel's reads are random 4-8 B
-gathers (one 64 B request per missing line), so FETCH_SIZE is used as is and
-the summary says so.
+Each *_DIR holds one `rocprofv3 --pmc ... --output-format csv -d DIR -o pmc`
+run of the same bench command (separate passes: FETCH_SIZE; WRITE_SIZE;
+TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum).  Every measurement line of the
+bench JSON (headline and secondaries) that carries `roofline.pmc_tag` and
+`roofline.pmc_match` {kernel regex, grid threads or null} gets an entry keyed
+by the tag, with the library sha the bench reports, so bench.py quotes it only
+for that exact build and workload size:
+
+  fetch/write_bytes_per_launch   FETCH_SIZE / WRITE_SIZE (KiB) x 1024, mean over
+                                 the matching dispatches
+  fabric_read_requests_per_launch  TCC_EA0_RDREQ_sum
+  hbm_bytes_per_launch           2 x FETCH_SIZE + WRITE_SIZE: FETCH_SIZE tallies
+                                 64 B per read request (FETCH_SIZE ==
+                                 TCC_EA0_RDREQ x 64 B), while a request moves a
+                                 128 B line (MI355X_MICROARCH.md §HBM gfx950
+                                 correction; profiles/calib_r02.json: a random
+                                 128 B block costs one request, 256 B two).
+                                 Infinity-Cache hits are counted (same guide).
 """
 import csv
+import glob
 import json
 import os
+import re
 import sys
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-def per_kernel(path, counter):
-    acc = {}
-    for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter:
-            continue
-        k = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
-        acc.setdefault(k, []).append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+def norm(name):
+    return name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0].strip()
+
+
+def rows(d):
+    out = []
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        out += list(csv.DictReader(open(f)))
+    return out
+
+
+def mean_counter(rs, counter, kre, grid):
+    v = [float(r["Counter_Value"]) for r in rs
+         if r["Counter_Name"] == counter and re.match(kre, norm(r["Kernel_Name"]))
+         and (grid is None or int(r.get("Grid_Size", -1)) == grid)]
+    return (sum(v) / len(v), len(v)) if v else (None, 0)
+
+
+def lines(bench):
+    yield bench.get("roofline") or {}
+    for v in (bench.get("secondary") or {}).values():
+        yield (v or {}).get("roofline") or {}
+        for m in (v or {}).get("more", []) or []:
+            yield m.get("roofline") or {}
 
 
 def main():
-    tag, fcsv, wcsv, bjson = sys.argv[1:5]
-    f = per_kernel(fcsv, "FETCH_SIZE")
-    w = per_kernel(wcsv, "WRITE_SIZE")
-    lines = per_kernel(sys.argv[5], "TCC_EA0_RDREQ_sum") if len(sys.argv) > 5 else {}
-    hits = per_kernel(sys.argv[5], "TCC_HIT_sum") if len(sys.argv) > 5 else {}
-    miss = per_kernel(sys.argv[5], "TCC_MISS_sum") if len(sys.argv) > 5 else {}
-    bench = json.load(open(bjson))
-    out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
-                            "pmc_summary.json")
+    fdir, wdir, rdir, bjson = sys.argv[1:5]
+    bench = [json.loads(ln) for ln in open(bjson) if ln.startswith("{")][-1]
+    sha = (bench.get("roofline") or {}).get("lib_sha256")
+    F, W, R = rows(fdir), rows(wdir), rows(rdir)
+    out_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         summ = json.load(open(out_path))
     except Exception:
         summ = {}
-    roof = bench["roofline"]
-    walk_key = [k for k in f if k.startswith("k_walk_scale") or k.startswith("k_walk_bitset")][0]
-    fb, wb = f[walk_key] * 1024, w[walk_key] * 1024
-    summ[tag] = {
-        "kernel": walk_key,
-        "walk_steps_per_launch": roof["units_per_launch"],
-        "lib_sha256": roof.get("lib_sha256"),
-        "fetch_bytes_per_launch": fb,
-        "write_bytes_per_launch": wb,
-        "hbm_bytes_per_launch": fb + wb,
-        "algorithmic_bytes_per_launch": roof["bytes_per_unit"] * roof["units_per_launch"],
-        "fetch_bytes_per_step": fb / roof["units_per_launch"],
-        "write_bytes_per_step": wb / roof["units_per_launch"],
-        "fabric_read_requests_per_launch": lines.get(walk_key),
-        "l2_hit_rate": (hits[walk_key] / (hits[walk_key] + miss[walk_key])) if walk_key in hits else None,
-        "kernel_ms": roof.get("kernel_ms"),
-        "note": "FETCH_SIZE/WRITE_SIZE (KiB) x 1024, mean over dispatches, separate --pmc passes; "
-                "FETCH_SIZE not doubled (random gathers, not 16 B/lane streaming)",
-    }
-    ts = [k for k in f if k.startswith("k_topsim")]
-    if ts and bench.get("secondary"):
-        summ[tag]["topsim"] = {"kernel": ts[0], "fetch_bytes_per_launch": f[ts[0]] * 1024,
-                               "write_bytes_per_launch": w[ts[0]] * 1024}
+    for roof in lines(bench):
+        tag, m = roof.get("pmc_tag"), roof.get("pmc_match")
+        if not tag or not m:
+            continue
+        kre, grid = m["kernel"], m.get("grid")
+        fb, nf = mean_counter(F, "FETCH_SIZE", kre, grid)
+        wb, nw = mean_counter(W, "WRITE_SIZE", kre, grid)
+        rq, nr = mean_counter(R, "TCC_EA0_RDREQ_sum", kre, grid)
+        hit, _ = mean_counter(R, "TCC_HIT_sum", kre, grid)
+        miss, _ = mean_counter(R, "TCC_MISS_sum", kre, grid)
+        if fb is None or wb is None:
+            print(f"{tag}: no matching dispatches for {kre} grid {grid}", file=sys.stderr)
+            continue
+        units = roof.get("units_per_launch")
+        e = {
+            "kernel": kre, "grid": grid, "dispatches": [nf, nw, nr], "lib_sha256": sha,
+            "units_per_launch": units,
+            "fetch_bytes_per_launch": fb * 1024, "write_bytes_per_launch": wb * 1024,
+            "hbm_bytes_per_launch": 2 * fb * 1024 + wb * 1024,
+            "fabric_read_requests_per_launch": rq,
+            "l2_hit_rate": hit / (hit + miss) if hit is not None and miss and hit + miss > 0 else None,
+            "algorithmic_bytes_per_launch": roof.get("algorithmic_bytes") or (
+                roof.get("bytes_per_unit", 0) * (units or 0)),
+            "note": "2 x FETCH_SIZE + WRITE_SIZE (KiB x 1024), mean over matching dispatches of separate --pmc "
+                    "passes; FETCH_SIZE counts 64 B per 128 B read request (tools/pmc_summary.py)",
+        }
+        if units:
+            e["fabric_read_requests_per_unit"] = rq / units if rq else None
+            e["hbm_bytes_per_unit"] = e["hbm_bytes_per_launch"] / units
+        summ[tag] = e
+        print(tag, json.dumps({k: e[k] for k in ("units_per_launch", "hbm_bytes_per_launch",
+                                                 "fabric_read_requests_per_launch", "l2_hit_rate")}))
     json.dump(summ, open(out_path, "w"), indent=1)
-    print(json.dumps(summ[tag], indent=1))
 
 
 if __name__ == "__main__":
