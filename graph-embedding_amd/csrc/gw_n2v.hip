@@ -831,8 +831,11 @@ int gw_dev_n2v_walks_replay(gw_graph* g, int L, int64_t nwalks, const int32_t* s
       break;
     }
     // walks before mism used correct offsets; mism's own offset was correct
-    // too, so its length is final.  Re-plan everything after it.
-    for (int64_t w = first_unsettled; w <= mism; ++w) lens[w] = got[w];
+    // too, so its length is final.  Every later walk takes this pass's length
+    // as its next guess (not the full length again): a sink-heavy directed
+    // graph then converges in a few passes instead of one pass per walk that
+    // stops early, and the settled prefix still grows by >= 1 per pass.
+    for (int64_t w = first_unsettled; w < nwalks; ++w) lens[w] = got[w];
     first_unsettled = mism + 1;
     if (first_unsettled >= nwalks) {
       int64_t a2 = 0;

@@ -497,3 +497,42 @@ def test_calls_run_on_the_graph_device_and_keep_the_callers(gw, oracle):
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
     G.free()
     assert torch.cuda.current_device() == 0
+
+
+def test_replay_sink_heavy_directed_many_walks(gw, oracle):
+    """MT-replay on a directed graph where many walks stop at sinks (each one
+    shifts the uniform offsets of every later walk): 200 walks per vertex ==
+    the oracle's sequential replay, and the offset fixed point converges in a
+    few passes (one pass per early-stopping walk was O(walks^2))."""
+    import time
+    from gwamd import _lib as C
+    G = gw.GWGraph.from_edgelist(os.path.join(DATA, "directed_sinks.edgelist"), " ", "nx", True).to_device(0)
+    C.check(C.lib().gw_n2v_prepare(G.handle, 0.5, 2.0, C.N2V_REPLAY), G.handle)
+    csr = G.export_csr()
+    n, nnz = G.n, G.nnz
+    inf = G.info()
+    nJ = np.empty(nnz, np.int32)
+    nq = np.empty(nnz, np.float64)
+    eoff = np.empty(nnz + 1, np.int64)
+    C.check(C.lib().gw_n2v_export_alias(G.handle, C.ptr(nJ), C.ptr(nq), C.ptr(eoff), None, None), G.handle)
+    ne = int(eoff[-1])
+    eJ = np.empty(ne, np.int32)
+    eq = np.empty(ne, np.float64)
+    C.check(C.lib().gw_n2v_export_alias(G.handle, C.ptr(nJ), C.ptr(nq), C.ptr(eoff), C.ptr(eJ), C.ptr(eq)), G.handle)
+    L = 20
+    starts = np.tile(csr["node_order"], 200).astype(np.int32)
+    U = np.random.RandomState(9).random_sample(2 * (L - 1) * len(starts))
+    out = np.empty((len(starts), L), np.int32)
+    lens = np.empty(len(starts), np.int32)
+    used = C.I64(0)
+    t0 = time.perf_counter()
+    C.check(C.lib().gw_n2v_walks_replay(G.handle, L, len(starts), C.ptr(starts), C.ptr(U), len(U), C.ptr(out),
+                                        C.ptr(lens), C.ctypes.byref(used)), G.handle)
+    dt = time.perf_counter() - t0
+    ref, rl, rused = oracle.walks_replay(csr["offsets"], csr["nbrs"], nJ, nq, eoff, eJ, eq, L, starts, U)
+    assert (rl < L).sum() > len(starts) // 4  # sink-heavy: many walks stop early
+    np.testing.assert_array_equal(out, ref)
+    np.testing.assert_array_equal(lens, rl)
+    assert used.value == rused
+    assert dt < 20.0, dt
+    del inf
