@@ -397,6 +397,26 @@ def gather_timing(R, args, step, out, L, B):
 
 
 # ---- workloads -----------------------------------------------------------------
+def stream_copy_gbps(R, nbytes=4 << 30, reps=5):
+    """Achievable HBM bandwidth on this box: a device-to-device copy of
+    `nbytes` (read + write counted), best of `reps` (SURVEY §8d asks for the
+    streaming copy beside the 8 TB/s spec)."""
+    torch = R.torch
+    a = torch.empty(nbytes // 4, dtype=torch.int32, device=R.dev)
+    b = torch.empty_like(a)
+    a.fill_(1)
+    best = 0.0
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        torch.cuda.synchronize()
+        best = max(best, 2 * nbytes / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    del a, b
+    return best
+
+
 def walk_headline(R, args):
     """Headline node2vec measurement (configs 2 and 4)."""
     import numpy as np
@@ -540,6 +560,8 @@ def walk_headline(R, args):
         res["allgather_all_ranks_ok"] = bool(ok[0] >= 1.0)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_walks(G.export_csr(), args.p, args.q, args.seed, L, 0, args.cpu_seconds)
+    if rank == 0:
+        res["copy_gbps"] = stream_copy_gbps(R)
     del out
     G.free()
     return res
@@ -932,6 +954,8 @@ def main(argv):
                          "trials_per_step": "rejection_trials_per_step"}[k]] = head[k]
             res["roofline"] = head.get("roofline")
             res["cpu_baseline"] = cpu
+            if res["roofline"] is not None and R.rank == 0:
+                res["roofline"]["stream_copy_GBps"] = head.get("copy_gbps")
             if "allgather" in head:
                 res["allgather"] = head["allgather"]
                 res["allgather_all_ranks_ok"] = head["allgather_all_ranks_ok"]
