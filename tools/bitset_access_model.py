@@ -36,6 +36,11 @@ def philox(c0, c1, c2, c3, k0, k1):
     return c0, c1, c2, c3
 
 
+def index64(hi, lo, d):
+    """gw_index (csrc/gw_philox.h): floor((hi * 2^32 + lo) * d / 2^64)."""
+    return ((hi << 32 | lo) * d) >> 64
+
+
 def bounded(x, d):
     return (x * d) >> 32
 
@@ -102,7 +107,7 @@ def main():
             fset = set()
             if mode == "region":
                 for k in common:
-                    ulo = ((int(k) << 32) + d - 1) // d
+                    ulo = (int(k) << 32) // d  # high words y of the 64-bit draws with index k
                     uhi = (((int(k) + 1) << 32) + d - 1) // d - 1
                     for b in range(bounded(ulo, F), bounded(uhi, F) + 1):
                         fset.add(b)
@@ -131,7 +136,7 @@ def main():
                                 add("sectors_region_directory")
                         break
                     add("branch_other")
-                k = bounded(u[1], d)
+                k = index64(u[1], u[2], d)  # the kernel's 64-bit "other" draw (u.y:u.z)
                 if mode == "region" and k != kp and bounded(u[1], F) in fset:
                     add("sectors_region_membership_word")
                 if k != kp and k not in cset:
