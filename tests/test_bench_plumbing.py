@@ -28,22 +28,25 @@ def _run(args, env_extra=None, timeout=240):
     return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
 
 
-@pytest.mark.parametrize("limit", [None, 200_000])
-def test_bench_two_ranks_plumbing(limit):
+@pytest.mark.parametrize("ranks,limit", [(2, None), (2, 200_000), (4, None)])
+def test_bench_multi_rank_plumbing(ranks, limit):
     steps, scale, L, nw = 3, 8, 80, 10
     env = {"GW_BENCH_GATHER_LIMIT": str(limit)} if limit else None
-    rc, res, err = _run(["--gpus", "2", "--plumbing-check", "--scale", str(scale), "--steps", str(steps),
+    rc, res, err = _run(["--gpus", str(ranks), "--plumbing-check", "--scale", str(scale), "--steps", str(steps),
                          "--warmup", "1"], env)
     assert rc == 0, err[-2000:]
-    assert res["ranks"] == 2 and res["backend"] == "gloo"
+    assert res["ranks"] == ranks and res["backend"] == "gloo"
     assert res["n_gpus"] == 0 and "rehearsal" in res  # no GPU: never reported as a GPU count
     B = nw * (1 << scale)
-    assert res["config"]["walks_per_step"] == 2 * B
-    assert res["walk_steps"] == 2 * steps * B * (L - 1)
+    assert res["config"]["walks_per_step"] == ranks * B
+    assert res["walk_steps"] == ranks * steps * B * (L - 1)
     g = res["allgather"]
     assert g["check_last_rank_block_identical"] is True and res["allgather_all_ranks_ok"] is True
-    assert g["gathered_bytes_per_step_per_rank"] == B * L * 4
-    assert g["mode"] == ("whole" if limit is None else "ring of 312-row chunks")
+    assert g["gathered_bytes_per_step_per_rank"] == (ranks - 1) * B * L * 4
+    if limit is not None:
+        assert g["mode"] == f"ring of {limit // (ranks * L * 4)}-row chunks"
+    else:
+        assert g["mode"] == "whole"
 
 
 def test_bench_rank_count_mismatch_is_refused():
