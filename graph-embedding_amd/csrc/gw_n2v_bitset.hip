@@ -443,151 +443,64 @@ __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff
   }
 }
 
-// j-th set bit among `nw` words held in registers (constant indices only)
+// j-th set bit among `nw` words held in registers (constant indices only),
+// branch-free: with running popcounts S_t, the target word is T = #{t : S_t
+// <= j}; j - S_{T-1} is the rank inside it
 template <int NW>
 __device__ __forceinline__ int regs_select(const uint32_t* wd, uint32_t j) {
-  uint32_t x = 0;
-  int base = 0;
-  bool found = false;
+  uint32_t S = 0, T = 0, below = 0, x = wd[0];
 #pragma unroll
   for (int t = 0; t < NW; ++t) {
-    const uint32_t pc = (uint32_t)__popc(wd[t]);
-    if (!found) {
-      if (j < pc) {
-        x = wd[t];
-        base = 32 * t;
-        found = true;
-      } else {
-        j -= pc;
-      }
-    }
+    S += (uint32_t)__popc(wd[t]);
+    const bool le = S <= j;
+    T += le ? 1u : 0u;
+    below = le ? S : below;
+    if (t + 1 < NW) x = le ? wd[t + 1] : x;
   }
-  return base + word_select(x, j);
+  return 32 * (int)T + word_select(x, j - below);
 }
 
-// j-th set bit of an inline bitset (entry words, 8 B aligned; L2-resident)
-__device__ __forceinline__ int64_t inl_select(const uint32_t* __restrict__ w, uint32_t j) {
-  uint32_t wd[10];
-#pragma unroll
-  for (int t = 0; t < 5; ++t) {
-    const uint2 v = reinterpret_cast<const uint2*>(w)[t];
-    wd[2 * t] = v.x;
-    wd[2 * t + 1] = v.y;
-  }
-  return regs_select<10>(wd, j);
-}
-
-// j-th set bit of a region bitset (c set bits): the 512-bit block comes from
-// the directory by interpolation (set bits are spread over the row), then
-// the block is read as one 64 B sector and searched in registers.  Up to
-// kPDir blocks the directory is the entry's payload (registers, no read).
-template <class Dir>
-__device__ __forceinline__ int64_t dir_block(Dir dir, int64_t ndir, uint32_t c, uint32_t* j) {
-  int64_t g = (int64_t)((uint64_t)*j * (uint64_t)ndir / c);
-  if (g >= ndir) g = ndir - 1;
-  uint32_t lo = dir(g);
-  uint32_t hi = g + 1 < ndir ? dir(g + 1) : c;
-  while (lo > *j) {
-    --g;
-    hi = lo;
-    lo = dir(g);
-  }
-  while (hi <= *j) {
-    ++g;
-    lo = hi;
-    hi = g + 1 < ndir ? dir(g + 1) : c;
-  }
-  *j -= lo;
-  return g;
-}
-
-__device__ __forceinline__ uint32_t pick10(const uint32_t (&pl)[10], uint32_t idx);
-
-__device__ __forceinline__ int64_t bs_select(const uint32_t (&pl)[10], const uint32_t* __restrict__ h, int64_t d,
-                                             uint32_t c, uint32_t j) {
-  const int64_t ndir = bs_ndir(d);
-  int64_t g = 0;
-  if (ndir > kPDir)
-    g = dir_block([&](int64_t x) { return h[x]; }, ndir, c, &j);
-  else if (ndir > 0)
-    g = dir_block([&](int64_t x) { return (pick10(pl, 1 + (uint32_t)(x >> 1)) >> (16 * (x & 1))) & 0xFFFFu; }, ndir, c,
-                  &j);
-  const uint4* blk = reinterpret_cast<const uint4*>(h + bs_boff(d) + g * kBlk);
-  uint32_t wd[kBlk];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const uint4 v = blk[t];
-    wd[4 * t] = v.x;
-    wd[4 * t + 1] = v.y;
-    wd[4 * t + 2] = v.z;
-    wd[4 * t + 3] = v.w;
-  }
-  return g * kDirBits + regs_select<kBlk>(wd, j);
-}
-
-// pl[idx] for a per-lane idx without dynamic register indexing
+// pl[idx] for a per-lane idx < 10 without dynamic register indexing: a
+// select tree on the index bits (9 v_cndmask + 4 bit tests; a mask-OR over
+// all ten words costs ~30 VALU).  idx >= 10 returns some payload word.
 __device__ __forceinline__ uint32_t pick10(const uint32_t (&pl)[10], uint32_t idx) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int t = 0; t < 10; ++t) r |= pl[t] & (0u - (uint32_t)(idx == (uint32_t)t));
-  return r;
+  const bool b0 = idx & 1u, b1 = idx & 2u, b2 = idx & 4u, b3 = idx & 8u;
+  const uint32_t a0 = b0 ? pl[1] : pl[0], a1 = b0 ? pl[3] : pl[2], a2 = b0 ? pl[5] : pl[4];
+  const uint32_t a3 = b0 ? pl[7] : pl[6], a4 = b0 ? pl[9] : pl[8];
+  const uint32_t c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2;
+  const uint32_t e0 = b2 ? c1 : c0;
+  return b3 ? a4 : e0;
+}
+
+// 32 payload bits from bit position pos (pos < 320; bits past 320 are
+// unspecified, callers use only bits inside the payload)
+__device__ __forceinline__ uint32_t bits32(const uint32_t (&pl)[10], uint32_t pos) {
+  const uint32_t w = pos >> 5;
+  return __builtin_amdgcn_alignbit(pick10(pl, w + 1), pick10(pl, w), pos & 31u);
 }
 
 // ---- Elias-Fano payload ----------------------------------------------------
-// The payload words live in registers; dynamic word picks are mask-selects.
-// j-th one (ONE) / zero among the payload bits, from bit 0 (the high parts
-// come first, so the first c ones and the first U - c zeros are theirs)
-template <bool ONE>
-__device__ __forceinline__ int ef_select_bit(const uint32_t (&pl)[10], uint32_t j) {
-  uint32_t x = 0;
-  int base = 0;
-  bool found = false;
-#pragma unroll
-  for (int t = 0; t < 10; ++t) {
-    const uint32_t m = ONE ? pl[t] : ~pl[t];
-    const uint32_t pc = (uint32_t)__popc(m);
-    if (!found) {
-      if (j < pc) {
-        x = m;
-        base = 32 * t;
-        found = true;
-      } else {
-        j -= pc;
-      }
+// High parts (unary, U bits: c ones, U - c zeros) come first, then c low
+// parts of l bits.  Bucket h (elements with high part h) starts right after
+// the (h-1)-th zero; its elements are the run of ones from there, indices
+// e0 = s - h on.  k (high h, low k & (2^l - 1)) is a member iff one of the
+// bucket's low parts equals k's (they ascend, so the scan stops early).
+// lw = the 32 bits at U + e0 * l (already read by the caller).
+__device__ __forceinline__ bool ef_bucket_has(const uint32_t (&pl)[10], uint32_t U, uint32_t l, uint32_t s,
+                                              uint32_t e0, uint32_t k, uint32_t lw) {
+  const uint32_t hw = bits32(pl, s);  // the run of ones ends at a zero below U
+  const uint32_t run = hw == 0xFFFFFFFFu ? 32u : (uint32_t)__builtin_ctz(~hw);
+  if (l == 0) return run > 0;
+  const uint32_t mask = (1u << l) - 1u, lowk = k & mask;
+  uint32_t o = 0;
+  for (uint32_t i = 0; i < run; ++i) {
+    if (o + l > 32u) {  // window exhausted (long bucket or wide low parts)
+      lw = bits32(pl, U + (e0 + i) * l);
+      o = 0;
     }
-  }
-  return base + word_select(x, j);
-}
-__device__ __forceinline__ uint32_t ef_low(const uint32_t (&pl)[10], uint32_t U, uint32_t i, int l) {
-  if (l == 0) return 0u;
-  const uint32_t off = U + i * (uint32_t)l;
-  const uint32_t w = off >> 5, sh = off & 31;
-  const uint64_t v = ((uint64_t)pick10(pl, w + 1) << 32) | pick10(pl, w);
-  return (uint32_t)(v >> sh) & ((1u << l) - 1u);
-}
-__device__ __forceinline__ int64_t ef_select(const uint32_t (&pl)[10], uint32_t U, int l, uint32_t j) {
-  const int pos = ef_select_bit<true>(pl, j);
-  return ((int64_t)(uint32_t)(pos - (int)j) << l) | ef_low(pl, U, j, l);
-}
-__device__ __forceinline__ bool ef_has(const uint32_t (&pl)[10], uint32_t c, uint32_t U, int l, uint32_t k) {
-  const uint32_t h = k >> l, lowk = k & ((1u << l) - 1u);
-  if (h > U - c) return false;  // beyond the largest high part
-  // bucket h starts right after the (h-1)-th zero
-  const uint32_t s = h > 0 ? (uint32_t)ef_select_bit<false>(pl, h - 1) + 1 : 0u;
-  for (uint32_t q = s; q < U; ++q) {
-    if (!((pick10(pl, q >> 5) >> (q & 31)) & 1u)) break;
-    if (ef_low(pl, U, q - h, l) == lowk) return true;
-  }
-  return false;
-}
-
-// Elias-Fano membership of k (high part h) once bucket h's first bit s is
-// known: the ones from s on are bucket h's elements, indices q - h
-__device__ __forceinline__ bool ef_scan(const uint32_t (&pl)[10], uint32_t U, int l, uint32_t h, uint32_t s, uint32_t k) {
-  const uint32_t lowk = k & ((1u << l) - 1u);
-  for (uint32_t q = s; q < U; ++q) {
-    if (!((pick10(pl, q >> 5) >> (q & 31)) & 1u)) break;
-    if (ef_low(pl, U, q - h, l) == lowk) return true;
+    const uint32_t f = (lw >> o) & mask;
+    if (f >= lowk) return f == lowk;
+    o += l;
   }
   return false;
 }
@@ -752,29 +665,37 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
         // parts) or the (eh-1)-th zero (start of Elias-Fano bucket eh)
         const uint32_t eh = (uint32_t)k >> efl;
         const bool ef_mem = op == 2 && mode == BS_EF && eh <= efU - c;
+        int pos = 0;
         if ((op == 1 && (mode == BS_INLINE || mode == BS_EF)) || (ef_mem && eh > 0)) {
           const bool inv = op == 2;
           uint32_t wp[10];
 #pragma unroll
           for (int q = 0; q < 10; ++q) wp[q] = inv ? ~pl[q] : pl[q];
-          const int pos = regs_select<10>(wp, inv ? eh - 1 : j);
-          if (op == 1) {
-            k = mode == BS_INLINE ? (int64_t)pos
-                                  : (((int64_t)(uint32_t)(pos - (int)j) << efl) | ef_low(pl, efU, j, efl));
-            acc = true;
-          } else {
-            common = ef_scan(pl, efU, efl, eh, (uint32_t)pos + 1u, (uint32_t)k);
-          }
-        } else if (ef_mem) {
-          common = ef_scan(pl, efU, efl, 0u, 0u, (uint32_t)k);
+          pos = regs_select<10>(wp, inv ? eh - 1 : j);
         }
+        const uint32_t es = (ef_mem && eh > 0) ? (uint32_t)pos + 1u : 0u;  // first bit of bucket eh
+        // ONE 32-bit payload window per lane serves every mode: the j-th u16
+        // of a list, bit k of an inline bitset, the Elias-Fano low part j /
+        // the low parts of bucket eh, the region draw-filter bucket
+        const uint32_t fb = gw_bounded(u.y, bs_filt_buckets(ndir));
+        const uint32_t wpos = mode == BS_LIST     ? 16u * j
+                              : mode == BS_INLINE ? (uint32_t)k
+                              : mode == BS_EF     ? efU + (op == 1 ? j : es - eh) * (uint32_t)efl
+                                                  : 32u * bs_filt_word(ndir) + fb;
+        const uint32_t win = bits32(pl, wpos);
         if (op == 1) {
-          if (mode == BS_LIST) {
-            k = (int64_t)((pick10(pl, j >> 1) >> (16 * (j & 1))) & 0xFFFFu);
+          if (mode == BS_INLINE) {
+            k = (int64_t)pos;
             acc = true;
-          } else if (mode == BS_REGION) {
+          } else if (mode == BS_EF) {
+            k = ((int64_t)(uint32_t)(pos - (int)j) << efl) | (win & ((1u << efl) - 1u));
+            acc = true;
+          } else if (mode == BS_LIST) {
+            k = (int64_t)(win & 0xFFFFu);
+            acc = true;
+          } else {  // BS_REGION
             if (ndir > kPDir) {  // directory in the region: guess the block, verify next iteration
-              g = (int64_t)((float)j * (float)ndir / (float)c);
+              g = (int64_t)((float)j * (float)ndir * __builtin_amdgcn_rcpf((float)c));
               if (g >= ndir) g = ndir - 1;
               dw0 = hreg[g];
               dw1 = g + 1 < ndir ? hreg[g + 1] : 0u;
@@ -798,10 +719,11 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
           if (mode == BS_LIST) {
             common = list_has(pl, (uint32_t)k);
           } else if (mode == BS_INLINE) {
-            common = (pick10(pl, (uint32_t)(k >> 5)) >> (k & 31)) & 1u;
-          } else if (mode == BS_REGION && k != (int64_t)kp && trial < (1u << 24)) {
-            const uint32_t fb = gw_bounded(u.y, bs_filt_buckets(ndir));
-            if ((pick10(pl, bs_filt_word(ndir) + (fb >> 5)) >> (fb & 31)) & 1u) {  // maybe common: read the word
+            common = win & 1u;
+          } else if (mode == BS_EF) {
+            common = ef_mem && ef_bucket_has(pl, efU, (uint32_t)efl, es, es - eh, (uint32_t)k, win);
+          } else if (k != (int64_t)kp && trial < (1u << 24)) {  // BS_REGION
+            if (win & 1u) {  // the draw filter says maybe common: read the word
               sw = (kGwDiag && (P.diag & 8)) ? G.bs_region[((uint32_t)k >> 5) & 0xFFFFu]  // timing experiment: no TLB misses
                                 : hreg[(meta >> 16) * kBlk + (k >> 5)];
               sbit = (uint32_t)(k & 31);

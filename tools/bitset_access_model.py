@@ -45,10 +45,10 @@ def bounded(x, d):
     return (x * d) >> 32
 
 
-def mode_of(c, d, list_max=20, bits=320):
+def mode_of(c, d, list_max=20, bits=320, inline_bits=None):
     if c <= list_max and d < 65536:
         return "list"
-    if d <= bits:
+    if d <= (inline_bits or bits):
         return "inline"
     if c > 0:
         l = int(np.floor(np.log2(d // c))) if d // c > 0 else 0
@@ -68,6 +68,8 @@ def main():
     # filter buckets with / without an in-entry directory, in-entry directory limit
     ap.add_argument("--payload-bits", type=int, default=320)
     ap.add_argument("--list-max", type=int, default=20)
+    ap.add_argument("--inline-bits", type=int, default=None,
+                    help="inline bitsets up to this degree (default: --payload-bits)")
     ap.add_argument("--filter-dir", type=int, default=160)
     ap.add_argument("--filter-nodir", type=int, default=288)
     ap.add_argument("--pdir", type=int, default=8, help="directory blocks kept in the entry (0: none)")
@@ -101,7 +103,7 @@ def main():
             kp = int(np.searchsorted(row, prev))
             common = np.nonzero(np.isin(row, prow, assume_unique=True) & (row != prev))[0]
             c = len(common)
-            mode = mode_of(c, d, a.list_max, a.payload_bits)
+            mode = mode_of(c, d, a.list_max, a.payload_bits, a.inline_bits)
             ndir = (d + 511) // 512 if d > 512 else 0
             F = a.filter_dir if 0 < ndir <= a.pdir else a.filter_nodir
             fset = set()
