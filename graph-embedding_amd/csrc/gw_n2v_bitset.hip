@@ -800,18 +800,27 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
       ++len;
     }
     // flush of the ready walkers' 64 B chunks, cooperative like the loads:
-    // an instruction writes 16 whole sectors instead of a 16 B piece of 64
+    // an instruction writes 16 whole sectors instead of a 16 B piece of 64.
+    // The ready walkers are compacted first (each publishes its lane at its
+    // rank among them), so a flush takes ceil(ready / 16) rounds, not 4:
+    // walkers drift apart by their retries and region phases, so most
+    // flushes serve a few walkers
     const unsigned long long rm = __ballot(ready);
     if (rm && !(kGwDiag && (P.diag & 32))) {
       if (vec_ok) {
+        const int nready = __popcll(rm);
+        int32_t* ids = reinterpret_cast<int32_t*>(ex);  // the exchange buffer is free here
+        __builtin_amdgcn_wave_barrier();
+        if (ready)
+          ids[__builtin_amdgcn_mbcnt_hi((uint32_t)(rm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rm, 0u))] = lane;
         __builtin_amdgcn_wave_barrier();
         const int32_t* sw = &s_stage[wv][0][0];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = 16 * j + (lane >> 2), p4 = 4 * (lane & 3);
+        for (int j = 0; 16 * j < nready; ++j) {
+          const int q = 16 * j + (lane >> 2), p4 = 4 * (lane & 3);
+          const int r = ids[q < nready ? q : nready - 1];
           const int lr = __shfl(flen, r, 64);
           const int64_t ir = ((int64_t)__shfl((int)(i >> 32), r, 64) << 32) | (uint32_t)__shfl((int)i, r, 64);
-          if ((rm >> r) & 1ull) {
+          if (q < nready) {
             const int4 v = make_int4(sw[64 * p4 + r], sw[64 * (p4 + 1) + r], sw[64 * (p4 + 2) + r], sw[64 * (p4 + 3) + r]);
             *reinterpret_cast<int4*>(out + ir * (int64_t)L + (lr - (kStage - 1)) + p4) = v;
           }

@@ -91,8 +91,10 @@ def main():
     def add(key, v=1):
         cnt[key] = cnt.get(key, 0) + v
 
+    iters = np.zeros(a.walks)  # loop iterations each walk occupies (trials + region phases)
     for i in range(a.walks):
         w = begin + i
+        iters[i] = 1
         c0, c1 = w & M32, (w >> 32) & M32
         last_ret = False
         for t in range(2, int(lens[i])):
@@ -120,6 +122,7 @@ def main():
             while True:
                 u = philox(c0, c1, t, trial, k0, k1)
                 trial += 1
+                iters[i] += 1
                 if trial == 1:
                     Z = (ap_ + c) + (d - 1 - c) * aq
                     r = u[0] * 2.3283064365386963e-10 * Z
@@ -134,8 +137,10 @@ def main():
                         add("branch_common")
                         if mode == "region":
                             add("sectors_region_select_block")
+                            iters[i] += 1
                             if ndir > a.pdir:
                                 add("sectors_region_directory")
+                                iters[i] += 1
                         break
                     add("branch_other")
                 k = index64(u[1], u[2], d)  # the kernel's 64-bit "other" draw (u.y:u.z)
@@ -144,12 +149,17 @@ def main():
                 if k != kp and k not in cset:
                     break
                 add("other_retries")
+    # a wave's 64 lanes run until its slowest walk ends: lane occupancy
+    g = iters[: len(iters) // 64 * 64].reshape(-1, 64)
+    occupancy = float(g.mean() / g.max(axis=1).mean()) if len(g) else None
     res = {"graph": f"R-MAT-{a.scale}", "p": a.p, "q": a.q, "walks": a.walks, "steps_modelled": steps}
     for k, v in sorted(cnt.items()):
         res[k + "_per_step"] = v / steps
     extra = sum(v for k, v in cnt.items() if k.startswith("sectors_")) / steps
     res["extra_region_sectors_per_step"] = extra
     res["model_read_sectors_per_step"] = 1.0 + extra + 2.0 / L  # + entry; + walk starts (order, offsets)
+    res["iterations_per_walk_mean"] = float(iters.mean())
+    res["wave_lane_occupancy"] = occupancy
     try:
         pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))
         e = pmc[f"n2v_rmat{a.scale}_p{a.p}_q{a.q}_L80_r10_bitset"]

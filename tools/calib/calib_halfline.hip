@@ -12,6 +12,11 @@
 //      previous iteration (the candidate layout)
 //   2  a dword from an unrelated random line (control: one more request)
 //   3  as 1, but from the second half of the line read two iterations earlier
+//   4  the first 48 B of the line's second half fetched in the same
+//      iteration by LDS-DMA (global_load_lds_dwordx4: lanes 4m..4m+2 of a
+//      round, walker 16j+m's 64 B LDS record), one word of it folded into
+//      the next address (the candidate bitset-entry layout: 64 B header +
+//      payload in registers, 48 B extension in LDS)
 // The dword's value enters the next address, so it is a dependent read.
 //
 //   calib_halfline [--sizes MB,..] [--modes 0,1,2,3] [--waves 5] [--iters N]
@@ -45,6 +50,7 @@ template <int MODE>
 __global__ void __launch_bounds__(256) k_half(const uint4* __restrict__ buf, unsigned long long nline, int iters,
                                               unsigned* __restrict__ out) {
   extern __shared__ unsigned s_pad[];
+  __shared__ uint4 s_rec[4][64][4];  // MODE 4: per-wave 64 B records
   const unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const unsigned* bw = reinterpret_cast<const unsigned*>(buf);
@@ -65,9 +71,17 @@ __global__ void __launch_bounds__(256) k_half(const uint4* __restrict__ buf, uns
       const unsigned long long sj =
           ((unsigned long long)(unsigned)__shfl((int)shi, src, 64) << 32) | (unsigned)__shfl((int)slo, src, 64);
       const uint4 a = buf[sj * 8 + (lane % 4)];  // first 64 B of the 128 B line
+      if (MODE == 4 && (lane & 3) != 3)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(buf + sj * 8 + 4 + (lane & 3)),
+                                         &s_rec[threadIdx.x >> 6][16 * j][0], 16, 0, 0);
       acc += a.x ^ a.w;
       const unsigned v = (unsigned)__shfl((int)a.x, (lane % 16) * 4, 64);
       if (lane / 16 == j) mine = v;
+    }
+    if (MODE == 4) {
+      __builtin_amdgcn_s_waitcnt(0);  // the LDS-DMA writes have landed (vmcnt 0)
+      __builtin_amdgcn_wave_barrier();
+      extra = reinterpret_cast<const unsigned*>(&s_rec[threadIdx.x >> 6][lane][0])[(h >> 40) % 12];
     }
     prev2 = prev1;
     prev1 = s;
@@ -94,7 +108,7 @@ typedef void (*KFn)(const uint4*, unsigned long long, int, unsigned*);
 
 int main(int argc, char** argv) {
   std::vector<long long> sizes_mb = {8192};
-  std::vector<long long> modes = {0, 1, 2, 3};
+  std::vector<long long> modes = {0, 1, 2, 3, 4};
   std::vector<long long> waves = {5};
   int reps = 3, iters = 256;
   for (int i = 1; i < argc; ++i) {
@@ -118,13 +132,13 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  KFn fs[4] = {k_half<0>, k_half<1>, k_half<2>, k_half<3>};
+  KFn fs[5] = {k_half<0>, k_half<1>, k_half<2>, k_half<3>, k_half<4>};
   for (long long smb : sizes_mb)
     for (long long w : waves)
       for (long long m : modes) {
-        if (m < 0 || m > 3 || w < 1 || w > 8) continue;
+        if (m < 0 || m > 4 || w < 1 || w > 8) continue;
         KFn f = fs[m];
-        const size_t lds = (size_t)(160 * 1024 / w) & ~(size_t)1023;
+        const size_t lds = ((size_t)(160 * 1024 / w) & ~(size_t)1023) - 16384;  // + 16 KB static records
         if (lds > 64 * 1024) CK(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         const unsigned long long nline = ((unsigned long long)smb << 20) / 128ull;
         const int blocks = cus * (int)w;
