@@ -322,6 +322,7 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
              int shuffle, int32_t* __restrict__ out, int32_t* __restrict__ lens,
              unsigned long long* __restrict__ counters) {
   __shared__ int32_t s_stage[kBlock / 64][kStage][64];
+  __shared__ int32_t s_ids[kBlock / 64][64];  // flush: lanes of the ready walkers, by rank
   const int lane = threadIdx.x & 63;
   int32_t* stage = &s_stage[threadIdx.x >> 6][0][lane];  // slot j at stage[64*j]
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -460,20 +461,26 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
     }
     // flush: 64 contiguous bytes per ready walker.  Cooperative (like the
     // bitset kernel's loads): in round j lanes 4m..4m+3 store the four 16 B
-    // pieces of walker 16j+m's chunk, so an instruction writes 16 whole
-    // sectors instead of a 16 B piece of 64 (per-lane stores cost up to 22%
-    // of a launch: GW_DIAG_NO_STORE A/B)
+    // pieces of the chunk of the (16j+m)-th ready walker, so an instruction
+    // writes 16 whole sectors instead of a 16 B piece of 64 (per-lane stores
+    // cost up to 22% of a launch: GW_DIAG_NO_STORE A/B), and the ready
+    // walkers are compacted first: ceil(ready / 16) rounds, not 4
     const unsigned long long rm = __ballot(ready);
     if (rm && !(kGwDiag && P.diag)) {
       if (vec_ok) {
+        const int nready = __popcll(rm);
+        int32_t* ids = s_ids[threadIdx.x >> 6];
+        __builtin_amdgcn_wave_barrier();
+        if (ready)
+          ids[__builtin_amdgcn_mbcnt_hi((uint32_t)(rm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rm, 0u))] = lane;
         __builtin_amdgcn_wave_barrier();
         const int32_t* sw = &s_stage[threadIdx.x >> 6][0][0];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = 16 * j + (lane >> 2), p4 = 4 * (lane & 3);
+        for (int j = 0; 16 * j < nready; ++j) {
+          const int q = 16 * j + (lane >> 2), p4 = 4 * (lane & 3);
+          const int r = ids[q < nready ? q : nready - 1];
           const int lr = __shfl(flen, r, 64);
           const int64_t ir = ((int64_t)__shfl((int)(i >> 32), r, 64) << 32) | (uint32_t)__shfl((int)i, r, 64);
-          if ((rm >> r) & 1ull) {
+          if (q < nready) {
             const int4 v = make_int4(sw[64 * p4 + r], sw[64 * (p4 + 1) + r], sw[64 * (p4 + 2) + r], sw[64 * (p4 + 3) + r]);
             *reinterpret_cast<int4*>(out + ir * (int64_t)L + (lr - (kStage - 1)) + p4) = v;
           }
