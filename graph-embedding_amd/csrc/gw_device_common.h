@@ -34,6 +34,27 @@ __device__ __forceinline__ int64_t gw_row_find(const int32_t* __restrict__ nbrs,
   return (lo < e && nbrs[lo] == key) ? lo : -1;
 }
 
+// Exact neighbour sets for has_edge (GW_N2V_REJECTION): row r owns 2*deg(r)
+// int32 slots at 2*offsets[r] (load factor 1/2, linear probing from a
+// multiply-shift hash); a query reads one slot run, almost always inside one
+// 64 B sector (built by k_build_ehash, gw_n2v.hip).
+__device__ __forceinline__ uint32_t gw_eh_slot(int32_t key, uint32_t cap) {
+  return (uint32_t)(((uint64_t)((uint32_t)key * 0x9E3779B1u) * (uint64_t)cap) >> 32);
+}
+__device__ __forceinline__ bool gw_eh_has(const int32_t* __restrict__ eh, int64_t rb, int64_t re, int32_t key) {
+  const uint32_t cap = (uint32_t)(2 * (re - rb));
+  if (cap == 0) return false;
+  const int32_t* __restrict__ t = eh + 2 * rb;
+  uint32_t s = gw_eh_slot(key, cap);
+  for (uint32_t i = 0; i < cap; ++i) {
+    const int32_t k = t[s];
+    if (k == key) return true;
+    if (k == -1) return false;
+    s = s + 1 == cap ? 0u : s + 1;
+  }
+  return false;
+}
+
 // Sequential Vose/Walker alias construction exactly as node2vec.py:116-147:
 // q[k] = K*p_k; `smaller`/`larger` are LIFO lists filled in index order;
 // J[small] = large; q[large] = (q[large] + q[small]) - 1.0.

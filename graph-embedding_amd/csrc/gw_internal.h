@@ -193,8 +193,11 @@ int gw_dev_topsim_m(gw_graph* g, int variant, int capacity, int sample, int step
                     const int32_t* sources_dev, int64_t nsrc, int32_t* out_keys_dev, float* out_vals_dev,
                     int32_t* out_size_dev, int64_t* stats_dev, void* stream);
 int gw_dev_simrank_naive(gw_graph* g, double C, int iters, double* sim_dev, void* stream);
-int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes);
+int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only = false);
 int gw_dev_walk_bitset_launch(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int64_t walk_count,
+                              int shuffle, int32_t* out_dev, int32_t* len_dev, uint64_t* counters_dev,
+                              void* stream);
+int gw_dev_walk_listed_launch(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int64_t walk_count,
                               int shuffle, int32_t* out_dev, int32_t* len_dev, uint64_t* counters_dev,
                               void* stream);
 int gw_dev_n2v_walks(gw_graph* g, int walk_len, uint64_t seed,

@@ -227,29 +227,11 @@ __device__ __forceinline__ uint64_t gw_bm_bit(int64_t rowb, int64_t deg, int32_t
   return 16ull * (uint64_t)rowb + (((uint64_t)h * (uint64_t)(16 * deg)) >> 32);
 }
 
-// Exact neighbour sets for has_edge: row r owns 2*deg(r) int32 slots at
-// 2*offsets[r] (load factor 1/2, linear probing from a multiply-shift hash);
-// a query reads one slot run, almost always inside one 64 B sector, instead
-// of the bitmap line plus a log2(deg)-probe binary search.
-__device__ __forceinline__ uint32_t gw_eh_slot(int32_t key, uint32_t cap) {
-  return (uint32_t)(((uint64_t)((uint32_t)key * 0x9E3779B1u) * (uint64_t)cap) >> 32);
-}
-
+// Exact neighbour sets (gw_eh_has, gw_device_common.h) when built, else the
+// membership bitmap + binary search.
 __device__ __forceinline__ bool gw_has_edge(const gw_dev_graph& G, int64_t rb, int64_t re,
                                             int32_t key) {
-  if (G.eh) {
-    const uint32_t cap = (uint32_t)(2 * (re - rb));
-    if (cap == 0) return false;
-    const int32_t* __restrict__ t = G.eh + 2 * rb;
-    uint32_t s = gw_eh_slot(key, cap);
-    for (uint32_t i = 0; i < cap; ++i) {
-      const int32_t k = t[s];
-      if (k == key) return true;
-      if (k == -1) return false;
-      s = s + 1 == cap ? 0u : s + 1;
-    }
-    return false;
-  }
+  if (G.eh) return gw_eh_has(G.eh, rb, re, key);
   if (G.bitmap) {
     const uint64_t bit = gw_bm_bit(rb, re - rb, key);
     if (!((G.bitmap[bit >> 5] >> (bit & 31)) & 1u)) return false;
@@ -692,8 +674,29 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
   }
   dev_free(d.sent);
   const bool fo = (p == 1.0 && q == 1.0);
+  // rejection sampling on an unweighted undirected simple graph: 64 B listed
+  // entries (k_walk_listed) answer most has_edge(x, prev) probes from the
+  // payload of the entry that led to cur; when they do not fit (half the free
+  // HBM, < 2^32 slots) the 16 B slot entries below serve k_walk_scale
+  bool listed = false;
+  if (mode == GW_N2V_REJECTION && !fo && g->nnz && !g->weighted && !g->directed &&
+      g->semantics == GW_SEM_NX_SIMPLE && !GW_DIAG_ENV("GW_DIAG_NO_LISTS")) {
+    size_t fr = 0, tot = 0;
+    int64_t budget = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) budget = (int64_t)(fr / 2);
+    rc = gw_dev_bitset_build(g, budget, true);
+    if (rc == GW_OK) {
+      listed = true;
+    } else if (rc == GW_ERR_CAPACITY || rc == GW_ERR_NOMEM) {
+      gw_dev_bitset_release(g);
+      (void)hipGetLastError();
+      g->err.clear();
+    } else {
+      return rc;
+    }
+  }
   const char* nosent = GW_DIAG_ENV("GW_DIAG_NO_SENT");  // diagnostic A/B knob only
-  if ((mode == GW_N2V_REJECTION || fo) && g->nnz && !(nosent && nosent[0] == '1')) {
+  if ((mode == GW_N2V_REJECTION || fo) && !listed && g->nnz && !(nosent && nosent[0] == '1')) {
     // slot entries (16 B per slot, one dwordx4 per step) spare the candidate's
     // offsets[] read: +14% on R-MAT-24 ef 16 (p=1, q=0.5; 8.3 GB of entries),
     // so they are built whenever they fit in half of the free HBM
@@ -883,6 +886,9 @@ int gw_dev_n2v_walks(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int6
   }
   if (g->n2v_mode == GW_N2V_BITSET && !first_order)
     return gw_dev_walk_bitset_launch(g, L, seed, walk_begin, walk_count, shuffle, out_dev, len_dev, counters_dev,
+                                     stream);
+  if (g->n2v_mode == GW_N2V_REJECTION && !first_order && g->d.bs_nbr)
+    return gw_dev_walk_listed_launch(g, L, seed, walk_begin, walk_count, shuffle, out_dev, len_dev, counters_dev,
                                      stream);
   hipStream_t s = (hipStream_t)stream;
   const unsigned grid = grid_for(walk_count);

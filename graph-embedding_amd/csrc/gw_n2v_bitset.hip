@@ -84,6 +84,7 @@ __device__ __forceinline__ int32_t row_of_slot(const int64_t* __restrict__ off, 
 }
 
 __device__ __forceinline__ bool bs_has_edge(const gw_dev_graph& G, int64_t rb, int64_t re, int32_t key) {
+  if (G.eh) return gw_eh_has(G.eh, rb, re, key);
   if (G.bitmap) {
     const uint32_t h = (uint32_t)key * 0x9E3779B1u;
     const uint64_t bit = 16ull * (uint64_t)rb + (((uint64_t)h * (uint64_t)(16 * (re - rb))) >> 32);
@@ -345,11 +346,13 @@ __global__ void k_bs_count_wave(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn, con
 }
 
 // region words per slot: only slots whose payload is neither list, inline nor Elias-Fano
-__global__ void k_bs_sizes(gw_dev_graph G, const gw_bs_nbr* __restrict__ bsn, uint64_t* __restrict__ sz) {
+__global__ void k_bs_sizes(gw_dev_graph G, const gw_bs_nbr* __restrict__ bsn, uint64_t* __restrict__ sz,
+                           int lists_only) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= G.nnz) return;
   const uint32_t d = (uint32_t)G.deg[G.nbrs[e]];
-  sz[e] = (d > (uint32_t)GW_BS_INLINE_BITS && bs_mode(bsn[e].c, d) == BS_REGION) ? (uint64_t)bs_words(d) : 0ull;
+  sz[e] = (!lists_only && d > (uint32_t)GW_BS_INLINE_BITS && bs_mode(bsn[e].c, d) == BS_REGION)
+              ? (uint64_t)bs_words(d) : 0ull;
 }
 
 // deg(v) <= kSmallD: one thread builds the whole entry (list or inline bitset)
@@ -395,7 +398,7 @@ __global__ void k_bs_fill_small(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn) {
 
 // pass 2, one thread per slot (deg(v) > kSmallD, shorter row <= kThreadMin)
 __global__ void k_bs_fill_thread(gw_dev_graph G, const uint64_t* __restrict__ roff, uint32_t* __restrict__ reg,
-                                 gw_bs_nbr* __restrict__ bsn) {
+                                 gw_bs_nbr* __restrict__ bsn, int lists_only) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= G.nnz) return;
   const int32_t v = G.nbrs[e];
@@ -406,6 +409,7 @@ __global__ void k_bs_fill_thread(gw_dev_graph G, const uint64_t* __restrict__ ro
   gw_bs_nbr* en = bsn + e;
   const uint32_t c = en->c;
   en->meta = bs_meta(c, (uint32_t)d);
+  if (lists_only && bs_mode(c, (uint32_t)d) == BS_REGION) return;  // no payload: the walk probes
   const BsEmit E = bs_emit(en, reg, roff, e, c, (uint32_t)d);
   if (E.mode == BS_LIST) {
     for (uint32_t t = c; t < 2 * 10; ++t) reinterpret_cast<uint16_t*>(en->w)[t] = 0xFFFFu;
@@ -423,7 +427,7 @@ __global__ void k_bs_fill_thread(gw_dev_graph G, const uint64_t* __restrict__ ro
 // pass 2, one wave per queued slot
 __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff, uint32_t* __restrict__ reg,
                                gw_bs_nbr* __restrict__ bsn, const int64_t* __restrict__ big,
-                               const unsigned long long* __restrict__ nbig) {
+                               const unsigned long long* __restrict__ nbig, int lists_only) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -432,6 +436,10 @@ __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff
     const int64_t e = big[i];
     gw_bs_nbr* en = bsn + e;
     const uint32_t c = en->c, d = en->d;
+    if (lists_only && bs_mode(c, d) == BS_REGION) {  // no payload: the walk probes
+      if (lane == 0) en->meta = bs_meta(c, d);
+      continue;
+    }
     const BsEmit E = bs_emit(en, reg, roff, e, c, d);
     if (E.mode == BS_LIST && lane >= (int)c && lane < 2 * 10) reinterpret_cast<uint16_t*>(en->w)[lane] = 0xFFFFu;
     if (E.mode == BS_REGION && lane == 0) en->w[0] = (uint32_t)(roff[e] / kBlk);
@@ -852,6 +860,212 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
   }
 }
 
+// ---- listed rejection sampler (GW_N2V_REJECTION, unweighted undirected) ----
+// k_walk_scale's exact sampler — the same Philox draws, envelope, outlier
+// return edge and acceptance tests, hence the same walks (oracle.walks_scale)
+// — with one change: the lazy has_edge(x, prev) probe is answered from the
+// payload of the entry that brought the walker to cur (the common neighbours
+// of prev and cur as positions in N(cur), gw_dev_bitset_build(lists_only))
+// whenever that payload is a list, an inline bitset or Elias-Fano; entries
+// whose common set would need a region carry none, and those steps probe
+// prev's neighbour hash as k_walk_scale does.  The candidate's 64 B entry is
+// fetched cooperatively (k_walk_bitset's loads, exchange and flush).
+struct LsParams {
+  double a_q, M, lo, extra, h_prev;
+  uint32_t k0, k1, pk0, pk1;
+};
+
+// k in the entry payload's common set (mode list / inline / Elias-Fano)
+__device__ __forceinline__ bool payload_has(const uint32_t (&pl)[10], uint32_t meta, uint32_t c, uint32_t k) {
+  const uint32_t mode = meta & 3u;
+  const uint32_t efl = (meta >> 2) & 31u, efU = (meta >> 7) & 511u;
+  if (mode == BS_LIST) return list_has(pl, k);
+  const uint32_t eh = k >> efl;
+  uint32_t es = 0;
+  if (mode == BS_EF && eh > 0) {  // bucket eh starts after the (eh-1)-th zero of the high parts
+    uint32_t wp[10];
+#pragma unroll
+    for (int q = 0; q < 10; ++q) wp[q] = ~pl[q];
+    es = (uint32_t)regs_select<10>(wp, eh - 1) + 1u;
+  }
+  const uint32_t win = bits32(pl, mode == BS_INLINE ? k : efU + (es - eh) * efl);
+  if (mode == BS_INLINE) return win & 1u;
+  return eh <= efU - c && ef_bucket_has(pl, efU, efl, es, es - eh, k, win);
+}
+
+__global__ void __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(5, 5)))
+k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t walk_count, int shuffle,
+              int32_t* __restrict__ out, int32_t* __restrict__ lens, unsigned long long* __restrict__ counters) {
+  __shared__ int32_t s_stage[kB / 64][kStage][64];
+  __shared__ uint4 s_ex[kB / 64][64];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  int32_t* stage = &s_stage[wv][0][lane];
+  uint4* ex = s_ex[wv];
+  const uint4* __restrict__ ents = reinterpret_cast<const uint4*>(G.bs_nbr);
+
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = i < walk_count;
+  unsigned long long my_steps = 0, my_trials = 0;
+  const int64_t w = walk_begin + (valid ? i : 0);
+  int32_t cur = -1, prev = -1;
+  int len = L;
+  if (valid) {
+    const uint64_t it = (uint64_t)w / (uint64_t)G.n;
+    const uint64_t pos = (uint64_t)w % (uint64_t)G.n;
+    const uint64_t sp = shuffle ? gw_feistel_perm(pos, (uint64_t)G.n, P.pk0, P.pk1, (uint32_t)it) : pos;
+    cur = G.order[sp];
+    len = 1;
+  }
+  const bool vec_ok = (L & 3) == 0;
+  const uint32_t c0 = (uint32_t)w, c1 = (uint32_t)((uint64_t)w >> 32);
+  stage[0] = cur;
+  uint32_t trial = 0;
+  uint32_t b = 0, d = 0, pb = 0, pd = 0;  // rows of cur and prev (slot indices < 2^32)
+  if (valid) {
+    b = (uint32_t)G.offsets[cur];
+    d = (uint32_t)(G.offsets[cur + 1] - G.offsets[cur]);
+  }
+  uint32_t meta = BS_REGION, c = 0;  // payload of the entry (prev -> cur); BS_REGION: none, probe
+  uint32_t pl[10];
+#pragma unroll
+  for (int t = 0; t < 10; ++t) pl[t] = 0u;
+  for (;;) {
+    const bool active = len < L && d != 0;
+    if (__ballot(active) == 0ull) break;
+    uint64_t sec = 0ull;  // the candidate's entry
+    uint32_t k = 0;
+    double t = 0.0;
+    bool ret = false;  // outlier return to prev (no entry read)
+    if (active) {
+      if (len == 1) {  // first order (node2vec.py:28-29)
+        const gw_u4 u = gw_philox(c0, c1, 1u, 0u, P.k0, P.k1);
+        trial = 1;
+        k = gw_index(u.x, u.z, d);
+      } else {
+        const gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
+        ++trial;
+        const double A = P.M * (double)d + P.extra;
+        if (P.extra > 0.0 && gw_u01(u.z) * A < P.extra) {
+          ret = true;
+        } else {
+          k = gw_index(u.x, u.y, d);
+          t = gw_u01(u.w) * P.M;
+        }
+      }
+      if (!ret) sec = (uint64_t)(ents + (uint64_t)(b + k) * 4u);
+    }
+    const uint4 r0 = coop_piece(sec, lane, 0), r1 = coop_piece(sec, lane, 1);
+    const uint4 r2 = coop_piece(sec, lane, 2), r3 = coop_piece(sec, lane, 3);
+    uint32_t E[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      __builtin_amdgcn_wave_barrier();
+      if ((lane & 3) == q) {
+        ex[lane >> 2] = r0;
+        ex[16 + (lane >> 2)] = r1;
+        ex[32 + (lane >> 2)] = r2;
+        ex[48 + (lane >> 2)] = r3;
+      }
+      __builtin_amdgcn_wave_barrier();
+      const uint4 v = ex[lane];
+      E[4 * q] = v.x;
+      E[4 * q + 1] = v.y;
+      E[4 * q + 2] = v.z;
+      E[4 * q + 3] = v.w;
+    }
+    __builtin_amdgcn_wave_barrier();
+    bool acc = ret;
+    if (sec != 0ull) {
+      const int32_t next = (int32_t)E[0];
+      if (len == 1) {
+        acc = true;
+      } else if (next == prev) {
+        acc = t < P.h_prev;
+      } else if (t < P.lo) {
+        acc = true;
+      } else {
+        const bool adj = (meta & 3u) != BS_REGION ? payload_has(pl, meta, c, k)
+                                                  : bs_has_edge(G, pb, (int64_t)pb + pd, next);  // x in N(prev)
+        acc = t < (adj ? 1.0 : P.a_q);
+      }
+      if (trial >= (1u << 24)) acc = true;
+    }
+    bool ready = false;
+    int flen = 0;
+    if (acc) {
+      my_trials += trial;
+      trial = 0;
+      const int32_t next = ret ? prev : (int32_t)E[0];
+      const uint32_t ob = pb, od = pd;
+      prev = cur;
+      pb = b;
+      pd = d;
+      cur = next;
+      if (ret) {  // back over the same edge: the old prev's row, no payload for (cur -> prev)
+        b = ob;
+        d = od;
+        meta = BS_REGION;
+      } else {
+        d = E[1];
+        b = E[2];
+        meta = E[3];
+        c = E[5];
+#pragma unroll
+        for (int q = 0; q < 10; ++q) pl[q] = E[6 + q];
+      }
+      stage[64 * (len & (kStage - 1))] = cur;
+      ready = (len & (kStage - 1)) == kStage - 1;
+      flen = len;
+      ++len;
+    }
+    const unsigned long long rm = __ballot(ready);
+    if (rm) {
+      if (vec_ok) {
+        const int nready = __popcll(rm);
+        int32_t* ids = reinterpret_cast<int32_t*>(ex);
+        __builtin_amdgcn_wave_barrier();
+        if (ready)
+          ids[__builtin_amdgcn_mbcnt_hi((uint32_t)(rm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rm, 0u))] = lane;
+        __builtin_amdgcn_wave_barrier();
+        const int32_t* sw = &s_stage[wv][0][0];
+        for (int j = 0; 16 * j < nready; ++j) {
+          const int q = 16 * j + (lane >> 2), p4 = 4 * (lane & 3);
+          const int r = ids[q < nready ? q : nready - 1];
+          const int lr = __shfl(flen, r, 64);
+          const int64_t ir = ((int64_t)__shfl((int)(i >> 32), r, 64) << 32) | (uint32_t)__shfl((int)i, r, 64);
+          if (q < nready) {
+            const int4 v = make_int4(sw[64 * p4 + r], sw[64 * (p4 + 1) + r], sw[64 * (p4 + 2) + r], sw[64 * (p4 + 3) + r]);
+            *reinterpret_cast<int4*>(out + ir * (int64_t)L + (lr - (kStage - 1)) + p4) = v;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      } else if (ready) {
+        int32_t* dst = out + i * (int64_t)L + (flen - (kStage - 1));
+        for (int j = 0; j < kStage; ++j) dst[j] = stage[64 * j];
+      }
+    }
+  }
+  if (valid) {
+    int32_t* row = out + i * (int64_t)L;
+    const int base = len & ~(kStage - 1);
+    for (int t = base; t < len; ++t) row[t] = stage[64 * (t - base)];
+    for (int t = len; t < L; ++t) row[t] = -1;
+    if (lens) lens[i] = len;
+    my_steps = (unsigned long long)(len - 1);
+  }
+  if (counters) {
+    for (int off = 32; off > 0; off >>= 1) {
+      my_steps += __shfl_down(my_steps, off, 64);
+      my_trials += __shfl_down(my_trials, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&counters[0], my_steps);
+      atomicAdd(&counters[1], my_trials);
+    }
+  }
+}
+
 template <typename T>
 int bs_alloc(gw_graph* g, T** p, int64_t count) {
   *p = nullptr;
@@ -878,10 +1092,13 @@ void gw_dev_bitset_release(gw_graph* g) {
   bs_free(g->d.bs_nbr);
 }
 
-// Build the per-edge entries and regions.  Requires the membership bitmap
-// (has_edge).  Regions are sized from the exact common-neighbour counts (pass
-// 1), so slots whose payload fits the entry take no region space.
-int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes) {
+// Build the per-edge entries and regions.  Uses the membership bitmap
+// (has_edge) when present.  Regions are sized from the exact common-neighbour
+// counts (pass 1), so slots whose payload fits the entry take no region space.
+// lists_only: no regions at all — entries whose payload would need one keep
+// mode BS_REGION and no payload (the rejection sampler's listed entries,
+// k_walk_listed, probes for those).
+int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
   gw_dev_graph& d = g->d;
   gw_dev_bitset_release(g);
   const int64_t nnz = g->nnz;
@@ -919,7 +1136,7 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes) {
   GW_HIP_TRY(hipGetLastError());
   k_bs_count_wave<<<4096, kB>>>(d, d.bs_nbr, big, nbig);
   GW_HIP_TRY(hipGetLastError());
-  k_bs_sizes<<<grid, kB>>>(d, d.bs_nbr, sz);
+  k_bs_sizes<<<grid, kB>>>(d, d.bs_nbr, sz, lists_only ? 1 : 0);
   GW_HIP_TRY(hipGetLastError());
   GW_HIP_TRY(hipMemset(sz + nnz, 0, sizeof(uint64_t)));
   size_t tmpb = 0;
@@ -953,9 +1170,9 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes) {
   GW_HIP_TRY(hipMemset(d.bs_region, 0, (size_t)words * 4));
   k_bs_fill_small<<<grid, kB>>>(d, d.bs_nbr);
   GW_HIP_TRY(hipGetLastError());
-  k_bs_fill_thread<<<grid, kB>>>(d, roff, d.bs_region, d.bs_nbr);
+  k_bs_fill_thread<<<grid, kB>>>(d, roff, d.bs_region, d.bs_nbr, lists_only ? 1 : 0);
   GW_HIP_TRY(hipGetLastError());
-  k_bs_fill_wave<<<4096, kB>>>(d, roff, d.bs_region, d.bs_nbr, big, nbig);
+  k_bs_fill_wave<<<4096, kB>>>(d, roff, d.bs_region, d.bs_nbr, big, nbig, lists_only ? 1 : 0);
   GW_HIP_TRY(hipGetLastError());
   GW_HIP_TRY(hipDeviceSynchronize());
   cleanup();
@@ -978,6 +1195,27 @@ int gw_dev_walk_bitset_launch(gw_graph* g, int L, uint64_t seed, int64_t walk_be
   if (const char* ns = GW_DIAG_ENV("GW_DIAG_NO_STORE")) P.diag |= ns[0] == '1' ? 32u : 0u;
   const unsigned grid = (unsigned)std::max<int64_t>(1, (walk_count + kB - 1) / kB);
   k_walk_bitset<<<grid, kB, 0, (hipStream_t)stream>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev,
+                                                       len_dev, (unsigned long long*)counters_dev);
+  GW_HIP_TRY(hipGetLastError());
+  return GW_OK;
+}
+
+int gw_dev_walk_listed_launch(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int64_t walk_count,
+                              int shuffle, int32_t* out_dev, int32_t* len_dev, uint64_t* counters_dev,
+                              void* stream) {
+  LsParams P;
+  const double a_p = 1.0 / g->p;
+  P.a_q = 1.0 / g->q;
+  P.M = std::max(1.0, P.a_q);
+  P.lo = std::min(1.0, P.a_q);
+  P.extra = a_p > P.M ? a_p - P.M : 0.0;
+  P.h_prev = std::min(a_p, P.M);
+  P.k0 = (uint32_t)seed;
+  P.k1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_STEP;
+  P.pk0 = (uint32_t)seed;
+  P.pk1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_PERM;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, (walk_count + kB - 1) / kB);
+  k_walk_listed<<<grid, kB, 0, (hipStream_t)stream>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev,
                                                        len_dev, (unsigned long long*)counters_dev);
   GW_HIP_TRY(hipGetLastError());
   return GW_OK;

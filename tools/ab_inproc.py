@@ -19,6 +19,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "graph-embedding_amd"))
@@ -64,11 +65,19 @@ def main():
     steps = {}
     for rb in range(a.rebuild):
         hs = []
-        for L in libs:
+        for name, L in zip(a.libs, libs):
             h = ctypes.c_void_p()
             C.check(L.gw_graph_rmat(a.scale, a.ef, 0.57, 0.19, 0.19, 42, ctypes.byref(h)))
-            if L.gw_graph_to_device(h, 0) != 0 or L.gw_n2v_prepare(h, a.p, a.q, mode) != 0:
+            if L.gw_graph_to_device(h, 0) != 0:
                 raise SystemExit(L.gw_last_error(h).decode())
+            t0 = time.perf_counter()
+            if L.gw_n2v_prepare(h, a.p, a.q, mode) != 0:
+                raise SystemExit(L.gw_last_error(h).decode())
+            torch.cuda.synchronize()
+            inf = C.GraphInfo()
+            L.gw_graph_info(h, ctypes.byref(inf))
+            print(f"{name}: prepare {time.perf_counter() - t0:.2f} s, sampler tables {inf.sampler_bytes / 1e9:.2f} GB",
+                  file=sys.stderr, flush=True)
             hs.append(h)
         inf = C.GraphInfo()
         libs[0].gw_graph_info(hs[0], ctypes.byref(inf))
