@@ -375,6 +375,36 @@ def test_rejection_rmat_equals_oracle(gw, oracle, p, q):
     assert int(cnt[0]) == int(rc[0]) and int(cnt[1]) == int(rc[1])
 
 
+@pytest.mark.parametrize("graph", ["mixed", "hub"])
+@pytest.mark.parametrize("p,q", [(1, 0.5), (0.25, 4), (4, 0.25)])
+def test_rejection_listed_entries_equal_oracle(gw, oracle, tmp_path, graph, p, q):
+    """k_walk_listed (REJECTION on an unweighted undirected graph): the lazy
+    has_edge(x, prev) test answered from the list / inline / Elias-Fano
+    payload of the entry that led to cur, region-size common sets and the
+    outlier return (p < 1, no entry read) falling back to the neighbour-hash
+    probe — the same walks as k_walk_scale, i.e. the oracle's walks_scale."""
+    import torch
+    from gwamd import _lib as C
+    path = str(tmp_path / f"{graph}.edgelist")
+    (_mixed_mode_edgelist if graph == "mixed" else _hub_edgelist)(path)
+    G = gw.GWGraph.from_edgelist(path, " ", "nx").to_device(0)
+    C.check(C.lib().gw_n2v_prepare(G.handle, float(p), float(q), C.N2V_REJECTION), G.handle)
+    info = G.info()
+    assert info.sampler_bytes >= info.nnz * 64  # listed 64 B entries built
+    L, begin, count = 30, 4 * G.n + 9, 12000
+    out = torch.empty((count, L), dtype=torch.int32, device="cuda")
+    lens = torch.empty(count, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    C.check(C.lib().gw_n2v_walks(G.handle, L, 31, begin, count, 1, C.ptr(out), C.ptr(lens), C.ptr(cnt), None),
+            G.handle)
+    torch.cuda.synchronize()
+    ref, rl, rc = oracle.walks_scale(dict(G.export_csr(), weights=None), p, q, 31, L, begin, count, nthreads=8)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    np.testing.assert_array_equal(lens.cpu().numpy(), rl)
+    assert int(cnt[0]) == int(rc[0]) and int(cnt[1]) == int(rc[1])
+    G.free()
+
+
 def test_native_comm_single_rank_allgather(gw):
     """gw_comm (RCCL loaded at run time): a one-rank communicator gathers
     int32 walk blocks and float64 score blocks unchanged."""
