@@ -513,7 +513,7 @@ def walk_headline(R, args):
     value = steps_total / el
     launch_steps = steps_local // args.steps
     achieved = BYTES_PER_STEP * launch_steps / (k_avg_ms * 1e-3) / 1e9
-    kname = "k_walk_bitset" if mode == "bitset" else "k_walk_scale"
+    kname = walk_kernel_name(mode, G)
     tag = f"n2v_rmat{args.scale}_ef{args.edge_factor}_p{args.p}_q{args.q}_L{L}_r{args.num_walks}_{mode}"
     prof = load_prof(tag, launch_steps)
     traffic = prof["hbm_bytes_per_launch"] if prof else None
@@ -567,6 +567,18 @@ def walk_headline(R, args):
     return res
 
 
+def walk_kernel_name(mode, G):
+    """The kernel a prepared graph's walks launch: the bitset sampler, the
+    listed rejection sampler (64 B slot entries, built for unweighted
+    undirected graphs when they fit) or k_walk_scale (16 B entries)."""
+    if mode == "bitset":
+        return "k_walk_bitset"
+    inf = G.info()
+    if mode == "rejection" and inf.sampler_bytes >= 64 * inf.nnz:
+        return "k_walk_listed"
+    return "k_walk_scale"
+
+
 def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejection=False, walks_per_node=1):
     """One launch of `walks_per_node` walks per node per rank on graph BG (weak)."""
     torch = R.torch
@@ -614,7 +626,7 @@ def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejectio
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu_b = cpu_baseline_walks(BG.export_csr(), wp, wq, args.seed, L, 0, 10.0, max_walks=2_000_000)
     del bout
-    kname = "k_walk_bitset" if bmode == "bitset" else "k_walk_scale"
+    kname = walk_kernel_name(bmode, BG)
     tag = f"n2v_rmat{scale}_ef{ef}_p{wp}_q{wq}_L{L}_r{walks_per_node}_{bmode}"
     prof = load_prof(tag, local_steps)
     sbytes = BG.info().sampler_bytes

@@ -926,18 +926,35 @@ k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t wal
     b = (uint32_t)G.offsets[cur];
     d = (uint32_t)(G.offsets[cur + 1] - G.offsets[cur]);
   }
-  uint32_t meta = BS_REGION, c = 0;  // payload of the entry (prev -> cur); BS_REGION: none, probe
+  // payload of the entry (prev -> cur): meta (mode, Elias-Fano l / U) with
+  // min(c, 0xFFFF) in bits 16..31; mode BS_REGION = none, has_edge probes
+  uint32_t meta = BS_REGION;
   uint32_t pl[10];
 #pragma unroll
   for (int t = 0; t < 10; ++t) pl[t] = 0u;
+  // A probe is pipelined: the candidate's entry is parked (header below, its
+  // payload in pl, which is unused while meta says BS_REGION) and the hash
+  // slot of prev's row is read in the NEXT iteration beside the other lanes'
+  // entry loads; the decision uses the draw kept in t.
+  bool pend = false;
+  int32_t px = 0;
+  uint32_t pdx = 0, poff = 0, pmeta = 0;
+  double t = 0.0;
   for (;;) {
     const bool active = len < L && d != 0;
     if (__ballot(active) == 0ull) break;
     uint64_t sec = 0ull;  // the candidate's entry
     uint32_t k = 0;
-    double t = 0.0;
     bool ret = false;  // outlier return to prev (no entry read)
-    if (active) {
+    // pending probe: first slot of px's run in prev's neighbour hash
+    uint32_t hcap = 0, hs = 0;
+    int32_t h0 = -1;
+    if (pend) {
+      hcap = 2u * pd;
+      hs = gw_eh_slot(px, hcap);
+      h0 = G.eh[2 * (uint64_t)pb + hs];
+    }
+    if (active && !pend) {
       if (len == 1) {  // first order (node2vec.py:28-29)
         const gw_u4 u = gw_philox(c0, c1, 1u, 0u, P.k0, P.k1);
         trial = 1;
@@ -975,8 +992,23 @@ k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t wal
       E[4 * q + 3] = v.w;
     }
     __builtin_amdgcn_wave_barrier();
-    bool acc = ret;
-    if (sec != 0ull) {
+    bool acc = ret, take = false;  // take: adopt the entry in E (else the parked one)
+    if (pend) {  // the probe's first slot arrived: finish the run (rarely more than one slot)
+      bool adj = h0 == px;
+      if (!adj && h0 != -1) {
+        for (uint32_t j = 1; j < hcap; ++j) {
+          hs = hs + 1 == hcap ? 0u : hs + 1;
+          const int32_t kk = G.eh[2 * (uint64_t)pb + hs];
+          if (kk == px) {
+            adj = true;
+            break;
+          }
+          if (kk == -1) break;
+        }
+      }
+      acc = t < (adj ? 1.0 : P.a_q) || trial >= (1u << 24);
+      pend = false;
+    } else if (sec != 0ull) {
       const int32_t next = (int32_t)E[0];
       if (len == 1) {
         acc = true;
@@ -984,19 +1016,28 @@ k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t wal
         acc = t < P.h_prev;
       } else if (t < P.lo) {
         acc = true;
+      } else if ((meta & 3u) != BS_REGION) {
+        acc = t < (payload_has(pl, meta, meta >> 16, k) ? 1.0 : P.a_q);
+      } else if (G.eh) {  // park the candidate, probe next iteration
+        pend = true;
+        px = next;
+        pdx = E[1];
+        poff = E[2];
+        pmeta = (E[3] & 0xFFFFu) | (min(E[5], 0xFFFFu) << 16);
+#pragma unroll
+        for (int q = 0; q < 10; ++q) pl[q] = E[6 + q];
       } else {
-        const bool adj = (meta & 3u) != BS_REGION ? payload_has(pl, meta, c, k)
-                                                  : bs_has_edge(G, pb, (int64_t)pb + pd, next);  // x in N(prev)
-        acc = t < (adj ? 1.0 : P.a_q);
+        acc = t < (bs_has_edge(G, pb, (int64_t)pb + pd, next) ? 1.0 : P.a_q);
       }
-      if (trial >= (1u << 24)) acc = true;
+      if (trial >= (1u << 24) && !pend) acc = true;
+      take = true;
     }
     bool ready = false;
     int flen = 0;
     if (acc) {
       my_trials += trial;
       trial = 0;
-      const int32_t next = ret ? prev : (int32_t)E[0];
+      const int32_t next = ret ? prev : take ? (int32_t)E[0] : px;
       const uint32_t ob = pb, od = pd;
       prev = cur;
       pb = b;
@@ -1006,13 +1047,16 @@ k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t wal
         b = ob;
         d = od;
         meta = BS_REGION;
-      } else {
+      } else if (take) {
         d = E[1];
         b = E[2];
-        meta = E[3];
-        c = E[5];
+        meta = (E[3] & 0xFFFFu) | (min(E[5], 0xFFFFu) << 16);
 #pragma unroll
         for (int q = 0; q < 10; ++q) pl[q] = E[6 + q];
+      } else {  // the parked entry (payload already in pl)
+        d = pdx;
+        b = poff;
+        meta = pmeta;
       }
       stage[64 * (len & (kStage - 1))] = cur;
       ready = (len & (kStage - 1)) == kStage - 1;
