@@ -71,7 +71,11 @@ extern "C" {
 #define GW_N2V_REPLAY 0
 /* scale mode: per-node alias only (or none when unweighted); second-order
  * bias by exact rejection sampling with the return edge as an outlier;
- * Philox4x32-10 keyed by (seed, walk, step, trial).                        */
+ * Philox4x32-10 keyed by (seed, walk, step, trial).  On unweighted undirected
+ * NX_SIMPLE graphs prepare also builds 64 B listed slot entries (common
+ * neighbours of each edge's endpoints when they fit 40 B) that answer most
+ * has_edge probes; they take 64 B per adjacency entry and are skipped (same
+ * walks, 16 B entries) when they exceed half of the free HBM.              */
 #define GW_N2V_REJECTION 1
 /* exact second-order sampling from per-edge common-neighbour bitsets (the
  * reference's per-edge alias tables compressed to 1 bit per entry, sum(deg^2)

@@ -72,6 +72,8 @@ def main():
                     help="inline bitsets up to this degree (default: --payload-bits)")
     ap.add_argument("--filter-dir", type=int, default=160)
     ap.add_argument("--filter-nodir", type=int, default=288)
+    ap.add_argument("--tail-list", type=int, default=0,
+                    help="what-if: entries with c <= this also carry their commons as positions in N(u)")
     ap.add_argument("--pdir", type=int, default=8, help="directory blocks kept in the entry (0: none)")
     a = ap.parse_args()
     import gwamd
@@ -146,6 +148,12 @@ def main():
                 k = index64(u[1], u[2], d)  # the kernel's 64-bit "other" draw (u.y:u.z)
                 if mode == "region" and k != kp and bounded(u[1], F) in fset:
                     add("sectors_region_membership_word")
+                    if a.tail_list:  # would the candidate's entry (cur -> x) carry a tail-indexed list?
+                        x = int(row[k])
+                        rx = nbrs[off[x]:off[x + 1]]
+                        cx = int(np.isin(rx, row, assume_unique=True).sum()) - int(cur in set(rx.tolist()))
+                        if cx <= a.tail_list and d < 65536:
+                            add("membership_word_answered_by_candidate_tail_list")
                 if k != kp and k not in cset:
                     break
                 add("other_retries")
