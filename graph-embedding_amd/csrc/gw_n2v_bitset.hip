@@ -121,6 +121,17 @@ __device__ __forceinline__ int word_select(uint32_t x, uint32_t j) {
 constexpr int kThreadMin = 64;  // slots whose shorter row is <= this: one thread, else one wave
 
 enum { BS_LIST = 0, BS_INLINE = 1, BS_EF = 2, BS_REGION = 3 };
+constexpr uint32_t kFiltL = 320;  // lists-only builds: a region-size common set leaves a 320-bucket draw filter
+
+// lists-only builds (k_walk_listed): for common position k of a slot whose
+// set needs a region, set the filter buckets of every draw (hi : lo) with
+// index k, bucket = hi * kFiltL >> 32 (the listed draw's high word is u.x)
+__device__ __forceinline__ void bs_filter_only(uint32_t* w, int64_t k, uint32_t d) {
+  const uint64_t ulo = ((uint64_t)k << 32) / d;
+  const uint64_t uhi = ((((uint64_t)k + 1) << 32) + d - 1) / d - 1;
+  const uint32_t b0 = (uint32_t)((ulo * kFiltL) >> 32), b1 = (uint32_t)((uhi * kFiltL) >> 32);
+  for (uint32_t b = b0; b <= b1; ++b) atomicOr(&w[b >> 5], 1u << (b & 31));
+}
 __device__ __forceinline__ int bs_mode(uint32_t c, uint32_t d) {
   return gw_bs_is_list(c, d) ? BS_LIST : d <= (uint32_t)GW_BS_INLINE_BITS ? BS_INLINE : gw_bs_is_ef(c, d) ? BS_EF : BS_REGION;
 }
@@ -409,7 +420,10 @@ __global__ void k_bs_fill_thread(gw_dev_graph G, const uint64_t* __restrict__ ro
   gw_bs_nbr* en = bsn + e;
   const uint32_t c = en->c;
   en->meta = bs_meta(c, (uint32_t)d);
-  if (lists_only && bs_mode(c, (uint32_t)d) == BS_REGION) return;  // no payload: the walk probes
+  if (lists_only && bs_mode(c, (uint32_t)d) == BS_REGION) {  // no payload: a draw filter, the walk probes
+    common_thread(G, S, [&](int64_t k, uint32_t, int64_t) { bs_filter_only(en->w, k, (uint32_t)d); });
+    return;
+  }
   const BsEmit E = bs_emit(en, reg, roff, e, c, (uint32_t)d);
   if (E.mode == BS_LIST) {
     for (uint32_t t = c; t < 2 * 10; ++t) reinterpret_cast<uint16_t*>(en->w)[t] = 0xFFFFu;
@@ -436,8 +450,10 @@ __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff
     const int64_t e = big[i];
     gw_bs_nbr* en = bsn + e;
     const uint32_t c = en->c, d = en->d;
-    if (lists_only && bs_mode(c, d) == BS_REGION) {  // no payload: the walk probes
+    if (lists_only && bs_mode(c, d) == BS_REGION) {  // no payload: a draw filter, the walk probes
       if (lane == 0) en->meta = bs_meta(c, d);
+      int64_t kl;
+      common_wave(G, bs_slot(G, e), [&](int64_t k, uint32_t, int64_t) { bs_filter_only(en->w, k, d); }, &kl);
       continue;
     }
     const BsEmit E = bs_emit(en, reg, roff, e, c, d);
@@ -940,6 +956,11 @@ k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t wal
   int32_t px = 0;
   uint32_t pdx = 0, poff = 0, pmeta = 0;
   double t = 0.0;
+  // a BS_REGION entry's pl is its draw filter (kFiltL buckets over the draw's
+  // high word u.x; a clear bucket proves the candidate is not common) until a
+  // parked candidate overwrites it
+  bool filt = false;
+  uint32_t fb = 0;
   for (;;) {
     const bool active = len < L && d != 0;
     if (__ballot(active) == 0ull) break;
@@ -968,6 +989,7 @@ k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t wal
         } else {
           k = gw_index(u.x, u.y, d);
           t = gw_u01(u.w) * P.M;
+          fb = (uint32_t)(((uint64_t)u.x * kFiltL) >> 32);
         }
       }
       if (!ret) sec = (uint64_t)(ents + (uint64_t)(b + k) * 4u);
@@ -1018,8 +1040,11 @@ k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t wal
         acc = true;
       } else if ((meta & 3u) != BS_REGION) {
         acc = t < (payload_has(pl, meta, meta >> 16, k) ? 1.0 : P.a_q);
+      } else if (filt && !((pick10(pl, fb >> 5) >> (fb & 31)) & 1u)) {
+        acc = t < P.a_q;  // the filter proves "not common"
       } else if (G.eh) {  // park the candidate, probe next iteration
         pend = true;
+        filt = false;  // pl now holds the parked payload
         px = next;
         pdx = E[1];
         poff = E[2];
@@ -1058,6 +1083,7 @@ k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t wal
         b = poff;
         meta = pmeta;
       }
+      filt = !ret && (meta & 3u) == BS_REGION;
       stage[64 * (len & (kStage - 1))] = cur;
       ready = (len & (kStage - 1)) == kStage - 1;
       flen = len;
