@@ -35,32 +35,37 @@ constexpr bool kGwDiag = false;
 //   bitmap   u32[16*nnz/32] has_edge membership pre-filter (BITSET build; REJECTION when eh does not fit)
 //   eh       int32[2*nnz] per-row open-addressing neighbour sets (REJECTION, p/q != 1)
 //   bs_*     per-edge common-neighbour bitsets (BITSET mode, sum(deg^2) bits)
-constexpr int GW_BS_INLINE_BITS = 320;  // bitsets of deg(x) <= this live inside the entry
-constexpr int GW_BS_LIST = 20;          // <= this many common neighbours: sorted u16 positions inline
+constexpr uint32_t GW_BS_PACK_D = 65536;  // deg(x) below this: kp and c share one word
 struct gw_bs_nbr {  // GW_N2V_BITSET: one 64 B entry (one HBM sector) per adjacency slot (u -> x)
   uint32_t x, d;                 // neighbour, deg(x)
   uint32_t off;                  // offsets[x] (this mode needs < 2^32 adjacency entries)
   uint32_t meta;                 // payload mode | Elias-Fano l << 2 | U << 7 | region dir blocks << 16
-  uint32_t kp, c;                // position of u in N(x), #common neighbours
-  uint32_t w[10];                // payload, by (c, d): c <= 20 && d < 65536: positions of the
-                                 // common neighbours (u16, ascending, 0xFFFF padded); else
-                                 // d <= 320: the bitset itself; else Elias-Fano positions when
-                                 // they fit in 320 bits; else w[0..1] = region word offset
+  uint32_t r[12];                // d < 65536: r[0] = kp | c << 16, r[1..11] = payload (352 bits);
+                                 // else r[0] = kp, r[1] = c, r[2..11] = payload (320 bits).
+                                 // kp = position of u in N(x), c = #common neighbours.  Payload,
+                                 // by (c, d): c <= 22 && d < 65536: positions of the common
+                                 // neighbours (u16, ascending, 0xFFFF padded); else d <= 352:
+                                 // the bitset itself; else Elias-Fano positions when they fit;
+                                 // else w[0] = region block index, directory, draw filter.
+                                 // (The build keeps r[0] = kp, r[1] = c until pass 2 packs.)
 };
 #if defined(__HIPCC__)
 #define GW_BS_HD __host__ __device__
 #else
 #define GW_BS_HD
 #endif
-GW_BS_HD inline bool gw_bs_is_list(uint32_t c, uint32_t d) { return c <= GW_BS_LIST && d < 65536u; }
+GW_BS_HD inline uint32_t gw_bs_pw(uint32_t d) { return d < GW_BS_PACK_D ? 11u : 10u; }  // payload words
+GW_BS_HD inline uint32_t gw_bs_bits(uint32_t d) { return 32u * gw_bs_pw(d); }            // payload bits
+GW_BS_HD inline bool gw_bs_is_list(uint32_t c, uint32_t d) { return c <= 22u && d < GW_BS_PACK_D; }
+GW_BS_HD inline bool gw_bs_is_inline(uint32_t d) { return d <= gw_bs_bits(d); }
 // Elias-Fano payload (neither list nor inline bitset): the unary high parts
 // (U = c + ((d-1)>>l) + 1 bits) first, then l low bits per position; fits
-// when U + c*l <= 320.  l = floor(log2(d / c)).
+// when U + c*l <= the payload bits.  l = floor(log2(d / c)).
 GW_BS_HD inline int gw_bs_ef_l(uint32_t c, uint32_t d) { return 31 - __builtin_clz(d / c); }
 GW_BS_HD inline bool gw_bs_is_ef(uint32_t c, uint32_t d) {
-  if (gw_bs_is_list(c, d) || d <= (uint32_t)GW_BS_INLINE_BITS || c == 0) return false;
+  if (gw_bs_is_list(c, d) || gw_bs_is_inline(d) || c == 0) return false;
   const int l = gw_bs_ef_l(c, d);
-  return (uint64_t)c * l + c + ((d - 1) >> l) + 1 <= (uint64_t)GW_BS_INLINE_BITS;  // U + c*l
+  return (uint64_t)c * l + c + ((d - 1) >> l) + 1 <= (uint64_t)gw_bs_bits(d);  // U + c*l
 }
 static_assert(sizeof(gw_bs_nbr) == 64, "bitset entry must be one 64 B sector");
 

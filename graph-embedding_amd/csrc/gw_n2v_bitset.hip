@@ -58,17 +58,15 @@ constexpr int kSmallD = 32;      // thread-per-slot fill up to this degree
 constexpr int kStage = 16;
 
 constexpr int kPDir = 8;         // region entries with <= this many directory blocks keep the directory in the entry
-constexpr uint32_t kFilt = 160;  // coarse filter buckets in a region entry (w[5..9]) ...
-constexpr uint32_t kFiltW = 288; // ... or w[1..9] when the entry holds no directory (d <= 512 or d > 4096)
 
 __host__ __device__ __forceinline__ int64_t bs_ndir(int64_t d) { return d > kDirBits ? (d + kDirBits - 1) / kDirBits : 0; }
 __host__ __device__ __forceinline__ int64_t bs_round(int64_t w) { return (w + kBlk - 1) / kBlk * kBlk; }
 // word offset of the bits inside a region (a directory kept in the region is padded to a block)
 __host__ __device__ __forceinline__ int64_t bs_boff(int64_t d) {
-  return (d <= GW_BS_INLINE_BITS || bs_ndir(d) <= kPDir) ? 0 : bs_round(bs_ndir(d));
+  return (gw_bs_is_inline((uint32_t)d) || bs_ndir(d) <= kPDir) ? 0 : bs_round(bs_ndir(d));
 }
 __host__ __device__ __forceinline__ int64_t bs_words(int64_t d) {
-  return d <= GW_BS_INLINE_BITS ? 0 : bs_boff(d) + bs_round((d + 31) / 32);
+  return gw_bs_is_inline((uint32_t)d) ? 0 : bs_boff(d) + bs_round((d + 31) / 32);
 }
 
 __device__ __forceinline__ int32_t row_of_slot(const int64_t* __restrict__ off, int64_t n, int64_t e) {
@@ -93,8 +91,11 @@ __device__ __forceinline__ bool bs_has_edge(const gw_dev_graph& G, int64_t rb, i
   return gw_row_find(G.nbrs, rb, re, key) >= 0;
 }
 
-// region entries: the draw filter's bucket count and first payload word
-__host__ __device__ __forceinline__ uint32_t bs_filt_buckets(int64_t ndir) { return (ndir > 0 && ndir <= kPDir) ? kFilt : kFiltW; }
+// region entries: the draw filter's bucket count (the payload words after
+// w[0] and the in-entry directory) and first payload word
+__host__ __device__ __forceinline__ uint32_t bs_filt_buckets(int64_t ndir, uint32_t d) {
+  return 32u * (gw_bs_pw(d) - ((ndir > 0 && ndir <= kPDir) ? 5u : 1u));
+}
 __host__ __device__ __forceinline__ uint32_t bs_filt_word(int64_t ndir) { return (ndir > 0 && ndir <= kPDir) ? 5u : 1u; }
 
 // position of the j-th (0-based) set bit of x (j < popc(x))
@@ -133,7 +134,7 @@ __device__ __forceinline__ void bs_filter_only(uint32_t* w, int64_t k, uint32_t 
   for (uint32_t b = b0; b <= b1; ++b) atomicOr(&w[b >> 5], 1u << (b & 31));
 }
 __device__ __forceinline__ int bs_mode(uint32_t c, uint32_t d) {
-  return gw_bs_is_list(c, d) ? BS_LIST : d <= (uint32_t)GW_BS_INLINE_BITS ? BS_INLINE : gw_bs_is_ef(c, d) ? BS_EF : BS_REGION;
+  return gw_bs_is_list(c, d) ? BS_LIST : gw_bs_is_inline(d) ? BS_INLINE : gw_bs_is_ef(c, d) ? BS_EF : BS_REGION;
 }
 
 // per-entry constants of the step kernel (no divisions per step):
@@ -279,7 +280,7 @@ struct BsEmit {
       // (y:z) with index k have y in [floor(k*2^32/d), ceil((k+1)*2^32/d) - 1]
       const uint64_t ulo = ((uint64_t)k << 32) / d;
       const uint64_t uhi = ((((uint64_t)k + 1) << 32) + d - 1) / d - 1;
-      const uint32_t F = bs_filt_buckets(ndir), w0 = bs_filt_word(ndir);
+      const uint32_t F = bs_filt_buckets(ndir, d), w0 = bs_filt_word(ndir);
       const uint32_t b0 = gw_bounded((uint32_t)ulo, F), b1 = gw_bounded((uint32_t)uhi, F);
       for (uint32_t b = b0; b <= b1; ++b) atomicOr(&w[w0 + (b >> 5)], 1u << (b & 31));
     }
@@ -296,11 +297,15 @@ struct BsEmit {
   }
 };
 
+// payload words and common count of an entry (d < 65536: r[0] = kp | c << 16)
+__device__ __forceinline__ uint32_t* bs_payload(gw_bs_nbr* en, uint32_t d) { return en->r + (d < GW_BS_PACK_D ? 1 : 2); }
+__device__ __forceinline__ uint32_t bs_c(const gw_bs_nbr* en, uint32_t d) { return d < GW_BS_PACK_D ? en->r[0] >> 16 : en->r[1]; }
+
 __device__ __forceinline__ BsEmit bs_emit(gw_bs_nbr* en, uint32_t* reg, const uint64_t* roff, int64_t e, uint32_t c,
                                           uint32_t d) {
   BsEmit E;
   E.mode = bs_mode(c, d);
-  E.w = en->w;
+  E.w = bs_payload(en, d);
   E.ndir = 0;
   E.dir = E.bits = nullptr;
   E.pdir = nullptr;
@@ -315,7 +320,7 @@ __device__ __forceinline__ BsEmit bs_emit(gw_bs_nbr* en, uint32_t* reg, const ui
     E.dir = reg + roff[e];
     E.bits = E.dir + bs_boff(d);
     if (E.ndir <= kPDir) {
-      E.pdir = reinterpret_cast<uint16_t*>(en->w + 1);
+      E.pdir = reinterpret_cast<uint16_t*>(E.w + 1);
       E.dir = nullptr;
     }
   }
@@ -340,7 +345,9 @@ __global__ void k_bs_count(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn, int64_t*
     big[atomicAdd(nbig, 1ull)] = e;
   gw_bs_nbr* en = bsn + e;
   *reinterpret_cast<uint4*>(en) = make_uint4((uint32_t)v, (uint32_t)d, (uint32_t)(uint64_t)vb, 0u);
-  *reinterpret_cast<uint2*>(&en->kp) = make_uint2(kp >= 0 ? (uint32_t)(kp - vb) : 0xFFFFFFFFu, c);
+  const uint32_t k32 = kp >= 0 ? (uint32_t)(kp - vb) : 0xFFFFFFFFu;
+  *reinterpret_cast<uint2*>(&en->r[0]) =
+      d < GW_BS_PACK_D ? make_uint2((k32 & 0xFFFFu) | (c << 16), 0u) : make_uint2(k32, c);  // c: 0 if queued
 }
 
 __global__ void k_bs_count_wave(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn, const int64_t* __restrict__ big,
@@ -352,7 +359,10 @@ __global__ void k_bs_count_wave(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn, con
     const int64_t e = big[i];
     int64_t kl;
     const uint32_t c = common_wave(G, bs_slot(G, e), [](int64_t, uint32_t, int64_t) {}, &kl);
-    if ((threadIdx.x & 63) == 0) bsn[e].c = c;
+    if ((threadIdx.x & 63) == 0) {
+      if (bsn[e].d < GW_BS_PACK_D) bsn[e].r[0] |= c << 16;
+      else bsn[e].r[1] = c;
+    }
   }
 }
 
@@ -362,7 +372,7 @@ __global__ void k_bs_sizes(gw_dev_graph G, const gw_bs_nbr* __restrict__ bsn, ui
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= G.nnz) return;
   const uint32_t d = (uint32_t)G.deg[G.nbrs[e]];
-  sz[e] = (!lists_only && d > (uint32_t)GW_BS_INLINE_BITS && bs_mode(bsn[e].c, d) == BS_REGION)
+  sz[e] = (!lists_only && !gw_bs_is_inline(d) && bs_mode(bs_c(bsn + e, d), d) == BS_REGION)
               ? (uint64_t)bs_words(d) : 0ull;
 }
 
@@ -375,34 +385,32 @@ __global__ void k_bs_fill_small(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn) {
   if (d > kSmallD) return;
   gw_bs_nbr en;
   en.x = (uint32_t)v;
-  en.kp = 0xFFFFFFFFu;
-  en.c = 0;
   en.d = (uint32_t)d;
   en.off = (uint32_t)vb;
   en.meta = 0;
 #pragma unroll
-  for (int t = 0; t < 10; ++t) en.w[t] = 0;
+  for (int t = 0; t < 12; ++t) en.r[t] = 0;
   const int32_t u = row_of_slot(G.offsets, G.n, e);
   const int64_t ub = G.offsets[u], ue = G.offsets[u + 1];
-  uint32_t word = 0, c = 0;
+  uint32_t word = 0, c = 0, kp = 0xFFFFu;
   for (int64_t k = 0; k < d; ++k) {
     const int32_t x = G.nbrs[vb + k];
     if (x == u) {
-      en.kp = (uint32_t)k;
+      kp = (uint32_t)k;
     } else if (bs_has_edge(G, ub, ue, x)) {
       word |= 1u << (k & 31);
       ++c;
     }
   }
-  en.c = c;
+  en.r[0] = kp | (c << 16);  // d <= 32: packed header, payload r[1..11]
   en.meta = bs_meta(c, (uint32_t)d);
   if (gw_bs_is_list(c, (uint32_t)d)) {  // sorted positions, 0xFFFF padded
-    uint16_t* lp = reinterpret_cast<uint16_t*>(en.w);
-    for (int t = 0; t < 2 * 10; ++t) lp[t] = 0xFFFFu;
+    uint16_t* lp = reinterpret_cast<uint16_t*>(en.r + 1);
+    for (int t = 0; t < 2 * 11; ++t) lp[t] = 0xFFFFu;
     int t = 0;
     for (uint32_t x = word; x; x &= x - 1) lp[t++] = (uint16_t)(__ffs(x) - 1);
   } else {
-    en.w[0] = word;  // inline bitset (d <= 32)
+    en.r[1] = word;  // inline bitset (d <= 32)
   }
   bsn[e] = en;
 }
@@ -418,17 +426,18 @@ __global__ void k_bs_fill_thread(gw_dev_graph G, const uint64_t* __restrict__ ro
   const BsSlot S = bs_slot(G, e);
   if (min(S.ue - S.ub, d) > kThreadMin) return;  // k_bs_fill_wave
   gw_bs_nbr* en = bsn + e;
-  const uint32_t c = en->c;
+  const uint32_t c = bs_c(en, (uint32_t)d);
+  uint32_t* w = bs_payload(en, (uint32_t)d);
   en->meta = bs_meta(c, (uint32_t)d);
   if (lists_only && bs_mode(c, (uint32_t)d) == BS_REGION) {  // no payload: a draw filter, the walk probes
-    common_thread(G, S, [&](int64_t k, uint32_t, int64_t) { bs_filter_only(en->w, k, (uint32_t)d); });
+    common_thread(G, S, [&](int64_t k, uint32_t, int64_t) { bs_filter_only(w, k, (uint32_t)d); });
     return;
   }
   const BsEmit E = bs_emit(en, reg, roff, e, c, (uint32_t)d);
   if (E.mode == BS_LIST) {
-    for (uint32_t t = c; t < 2 * 10; ++t) reinterpret_cast<uint16_t*>(en->w)[t] = 0xFFFFu;
+    for (uint32_t t = c; t < 2 * gw_bs_pw((uint32_t)d); ++t) reinterpret_cast<uint16_t*>(w)[t] = 0xFFFFu;
   } else if (E.mode == BS_REGION) {
-    en->w[0] = (uint32_t)(roff[e] / kBlk);  // regions are block aligned: 32-bit block index
+    w[0] = (uint32_t)(roff[e] / kBlk);  // regions are block aligned: 32-bit block index
   }
   int64_t klast = -1;
   common_thread(G, S, [&](int64_t k, uint32_t idx, int64_t kprev) {
@@ -449,16 +458,17 @@ __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff
   for (int64_t i = wave; i < total; i += nwaves) {
     const int64_t e = big[i];
     gw_bs_nbr* en = bsn + e;
-    const uint32_t c = en->c, d = en->d;
+    const uint32_t d = en->d, c = bs_c(en, d);
+    uint32_t* w = bs_payload(en, d);
     if (lists_only && bs_mode(c, d) == BS_REGION) {  // no payload: a draw filter, the walk probes
       if (lane == 0) en->meta = bs_meta(c, d);
       int64_t kl;
-      common_wave(G, bs_slot(G, e), [&](int64_t k, uint32_t, int64_t) { bs_filter_only(en->w, k, d); }, &kl);
+      common_wave(G, bs_slot(G, e), [&](int64_t k, uint32_t, int64_t) { bs_filter_only(w, k, d); }, &kl);
       continue;
     }
     const BsEmit E = bs_emit(en, reg, roff, e, c, d);
-    if (E.mode == BS_LIST && lane >= (int)c && lane < 2 * 10) reinterpret_cast<uint16_t*>(en->w)[lane] = 0xFFFFu;
-    if (E.mode == BS_REGION && lane == 0) en->w[0] = (uint32_t)(roff[e] / kBlk);
+    if (E.mode == BS_LIST && lane >= (int)c && lane < 2 * (int)gw_bs_pw(d)) reinterpret_cast<uint16_t*>(w)[lane] = 0xFFFFu;
+    if (E.mode == BS_REGION && lane == 0) w[0] = (uint32_t)(roff[e] / kBlk);
     if (lane == 0) en->meta = bs_meta(c, d);
     int64_t klast;
     common_wave(G, bs_slot(G, e), E, &klast);
@@ -484,23 +494,24 @@ __device__ __forceinline__ int regs_select(const uint32_t* wd, uint32_t j) {
   return 32 * (int)T + word_select(x, j - below);
 }
 
-// pl[idx] for a per-lane idx < 10 without dynamic register indexing: a
-// select tree on the index bits (9 v_cndmask + 4 bit tests; a mask-OR over
-// all ten words costs ~30 VALU).  idx >= 10 returns some payload word.
-__device__ __forceinline__ uint32_t pick10(const uint32_t (&pl)[10], uint32_t idx) {
+// pl[idx] for a per-lane idx < kPW without dynamic register indexing: a
+// select tree on the index bits (10 v_cndmask + 4 bit tests; a mask-OR over
+// all the words costs ~3 VALU per word).  idx >= kPW returns some payload word.
+constexpr int kPW = 11;  // payload registers: 11 words for d < 65536 (packed kp | c), else 10 + a zero word
+__device__ __forceinline__ uint32_t pickw(const uint32_t (&pl)[kPW], uint32_t idx) {
   const bool b0 = idx & 1u, b1 = idx & 2u, b2 = idx & 4u, b3 = idx & 8u;
   const uint32_t a0 = b0 ? pl[1] : pl[0], a1 = b0 ? pl[3] : pl[2], a2 = b0 ? pl[5] : pl[4];
   const uint32_t a3 = b0 ? pl[7] : pl[6], a4 = b0 ? pl[9] : pl[8];
-  const uint32_t c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2;
+  const uint32_t c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2, c2 = b1 ? pl[10] : a4;
   const uint32_t e0 = b2 ? c1 : c0;
-  return b3 ? a4 : e0;
+  return b3 ? c2 : e0;
 }
 
 // 32 payload bits from bit position pos (pos < 320; bits past 320 are
 // unspecified, callers use only bits inside the payload)
-__device__ __forceinline__ uint32_t bits32(const uint32_t (&pl)[10], uint32_t pos) {
+__device__ __forceinline__ uint32_t bits32(const uint32_t (&pl)[kPW], uint32_t pos) {
   const uint32_t w = pos >> 5;
-  return __builtin_amdgcn_alignbit(pick10(pl, w + 1), pick10(pl, w), pos & 31u);
+  return __builtin_amdgcn_alignbit(pickw(pl, w + 1), pickw(pl, w), pos & 31u);
 }
 
 // ---- Elias-Fano payload ----------------------------------------------------
@@ -510,7 +521,7 @@ __device__ __forceinline__ uint32_t bits32(const uint32_t (&pl)[10], uint32_t po
 // e0 = s - h on.  k (high h, low k & (2^l - 1)) is a member iff one of the
 // bucket's low parts equals k's (they ascend, so the scan stops early).
 // lw = the 32 bits at U + e0 * l (already read by the caller).
-__device__ __forceinline__ bool ef_bucket_has(const uint32_t (&pl)[10], uint32_t U, uint32_t l, uint32_t s,
+__device__ __forceinline__ bool ef_bucket_has(const uint32_t (&pl)[kPW], uint32_t U, uint32_t l, uint32_t s,
                                               uint32_t e0, uint32_t k, uint32_t lw) {
   const uint32_t hw = bits32(pl, s);  // the run of ones ends at a zero below U
   const uint32_t run = hw == 0xFFFFFFFFu ? 32u : (uint32_t)__builtin_ctz(~hw);
@@ -530,10 +541,10 @@ __device__ __forceinline__ bool ef_bucket_has(const uint32_t (&pl)[10], uint32_t
 }
 
 // k in the inline common-neighbour list (registers, constant indices)
-__device__ __forceinline__ bool list_has(const uint32_t (&pl)[10], uint32_t k) {
+__device__ __forceinline__ bool list_has(const uint32_t (&pl)[kPW], uint32_t k) {
   bool hit = false;
 #pragma unroll
-  for (int t = 0; t < 10; ++t) hit |= (pl[t] & 0xFFFFu) == k || (pl[t] >> 16) == k;
+  for (int t = 0; t < kPW; ++t) hit |= (pl[t] & 0xFFFFu) == k || (pl[t] >> 16) == k;
   return hit;
 }
 
@@ -543,6 +554,16 @@ struct BsParams {
   uint32_t diag;  // timing experiments only (GW_DIAG_BS): 1 = no select, 2 = no membership test,
                  // 4 = region blocks / 8 = region words read from a small hot area (wrong walks)
 };
+
+// an arrived entry's kp, c and payload (gw_bs_nbr: packed header when d < 65536)
+__device__ __forceinline__ void unpack_entry(const uint32_t (&E)[16], uint32_t* kp, uint32_t* c, uint32_t (&pl)[kPW]) {
+  const bool packed = E[1] < GW_BS_PACK_D;
+  *kp = packed ? (E[4] & 0xFFFFu) : E[4];
+  *c = packed ? (E[4] >> 16) : E[5];
+#pragma unroll
+  for (int q = 0; q < kPW - 1; ++q) pl[q] = packed ? E[5 + q] : E[6 + q];
+  pl[kPW - 1] = packed ? E[15] : 0u;
+}
 
 // round j of a cooperative entry load: lane l fetches 16 B piece (l & 3) of
 // the entry of the walker in lane 16 j + (l >> 2) (none if that walker
@@ -601,9 +622,9 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
     d = (uint32_t)(G.offsets[cur + 1] - G.offsets[cur]);
   }
   uint32_t c = 0, kp = 0, meta = 0;
-  uint32_t pl[10];  // entry payload
+  uint32_t pl[kPW];  // entry payload
 #pragma unroll
-  for (int t = 0; t < 10; ++t) pl[t] = 0xFFFFFFFFu;
+  for (int t = 0; t < kPW; ++t) pl[t] = 0xFFFFFFFFu;
   // Region reads are pipelined with the entry loads: every loop iteration is
   // ONE memory round trip for the wave.  A step that selects inside a region
   // spends extra iterations (directory words dw0/dw1: ph 1; the 64 B block:
@@ -692,16 +713,16 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
         int pos = 0;
         if ((op == 1 && (mode == BS_INLINE || mode == BS_EF)) || (ef_mem && eh > 0)) {
           const bool inv = op == 2;
-          uint32_t wp[10];
+          uint32_t wp[kPW];
 #pragma unroll
-          for (int q = 0; q < 10; ++q) wp[q] = inv ? ~pl[q] : pl[q];
-          pos = regs_select<10>(wp, inv ? eh - 1 : j);
+          for (int q = 0; q < kPW; ++q) wp[q] = inv ? ~pl[q] : pl[q];
+          pos = regs_select<kPW>(wp, inv ? eh - 1 : j);
         }
         const uint32_t es = (ef_mem && eh > 0) ? (uint32_t)pos + 1u : 0u;  // first bit of bucket eh
         // ONE 32-bit payload window per lane serves every mode: the j-th u16
         // of a list, bit k of an inline bitset, the Elias-Fano low part j /
         // the low parts of bucket eh, the region draw-filter bucket
-        const uint32_t fb = gw_bounded(u.y, bs_filt_buckets(ndir));
+        const uint32_t fb = gw_bounded(u.y, bs_filt_buckets(ndir, d));
         const uint32_t wpos = mode == BS_LIST     ? 16u * j
                               : mode == BS_INLINE ? (uint32_t)k
                               : mode == BS_EF     ? efU + (op == 1 ? j : es - eh) * (uint32_t)efl
@@ -806,10 +827,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
       d = E[1];
       b = E[2];
       meta = E[3];
-      kp = E[4];
-      c = E[5];
-#pragma unroll
-      for (int q = 0; q < 10; ++q) pl[q] = E[6 + q];
+      unpack_entry(E, &kp, &c, pl);
     }
     if (slot != 0xFFFFFFFFu) {
       my_trials += trial;
@@ -892,17 +910,17 @@ struct LsParams {
 };
 
 // k in the entry payload's common set (mode list / inline / Elias-Fano)
-__device__ __forceinline__ bool payload_has(const uint32_t (&pl)[10], uint32_t meta, uint32_t c, uint32_t k) {
+__device__ __forceinline__ bool payload_has(const uint32_t (&pl)[kPW], uint32_t meta, uint32_t c, uint32_t k) {
   const uint32_t mode = meta & 3u;
   const uint32_t efl = (meta >> 2) & 31u, efU = (meta >> 7) & 511u;
   if (mode == BS_LIST) return list_has(pl, k);
   const uint32_t eh = k >> efl;
   uint32_t es = 0;
   if (mode == BS_EF && eh > 0) {  // bucket eh starts after the (eh-1)-th zero of the high parts
-    uint32_t wp[10];
+    uint32_t wp[kPW];
 #pragma unroll
-    for (int q = 0; q < 10; ++q) wp[q] = ~pl[q];
-    es = (uint32_t)regs_select<10>(wp, eh - 1) + 1u;
+    for (int q = 0; q < kPW; ++q) wp[q] = ~pl[q];
+    es = (uint32_t)regs_select<kPW>(wp, eh - 1) + 1u;
   }
   const uint32_t win = bits32(pl, mode == BS_INLINE ? k : efU + (es - eh) * efl);
   if (mode == BS_INLINE) return win & 1u;
@@ -945,9 +963,9 @@ k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t wal
   // payload of the entry (prev -> cur): meta (mode, Elias-Fano l / U) with
   // min(c, 0xFFFF) in bits 16..31; mode BS_REGION = none, has_edge probes
   uint32_t meta = BS_REGION;
-  uint32_t pl[10];
+  uint32_t pl[kPW];
 #pragma unroll
-  for (int t = 0; t < 10; ++t) pl[t] = 0u;
+  for (int t = 0; t < kPW; ++t) pl[t] = 0u;
   // A probe is pipelined: the candidate's entry is parked (header below, its
   // payload in pl, which is unused while meta says BS_REGION) and the hash
   // slot of prev's row is read in the NEXT iteration beside the other lanes'
@@ -1040,29 +1058,31 @@ k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t wal
         acc = true;
       } else if ((meta & 3u) != BS_REGION) {
         acc = t < (payload_has(pl, meta, meta >> 16, k) ? 1.0 : P.a_q);
-      } else if (filt && !((pick10(pl, fb >> 5) >> (fb & 31)) & 1u)) {
+      } else if (filt && !((pickw(pl, fb >> 5) >> (fb & 31)) & 1u)) {
         acc = t < P.a_q;  // the filter proves "not common"
       } else if (G.eh) {  // park the candidate, probe next iteration
         pend = true;
-        filt = false;  // pl now holds the parked payload
+        filt = false;  // pl will hold the parked payload
         px = next;
-        pdx = E[1];
-        poff = E[2];
-        pmeta = (E[3] & 0xFFFFu) | (min(E[5], 0xFFFFu) << 16);
-#pragma unroll
-        for (int q = 0; q < 10; ++q) pl[q] = E[6 + q];
       } else {
         acc = t < (bs_has_edge(G, pb, (int64_t)pb + pd, next) ? 1.0 : P.a_q);
       }
       if (trial >= (1u << 24) && !pend) acc = true;
       take = true;
     }
+    if (take && (pend || acc)) {  // the arrived entry becomes the parked or the current one
+      uint32_t ekp, ec;
+      unpack_entry(E, &ekp, &ec, pl);
+      pdx = E[1];
+      poff = E[2];
+      pmeta = (E[3] & 0xFFFFu) | (min(ec, 0xFFFFu) << 16);
+    }
     bool ready = false;
     int flen = 0;
     if (acc) {
       my_trials += trial;
       trial = 0;
-      const int32_t next = ret ? prev : take ? (int32_t)E[0] : px;
+      const int32_t next = ret ? prev : take ? (int32_t)E[0] : px;  // (E[0] == px when parked)
       const uint32_t ob = pb, od = pd;
       prev = cur;
       pb = b;
@@ -1072,13 +1092,7 @@ k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t wal
         b = ob;
         d = od;
         meta = BS_REGION;
-      } else if (take) {
-        d = E[1];
-        b = E[2];
-        meta = (E[3] & 0xFFFFu) | (min(E[5], 0xFFFFu) << 16);
-#pragma unroll
-        for (int q = 0; q < 10; ++q) pl[q] = E[6 + q];
-      } else {  // the parked entry (payload already in pl)
+      } else {  // the arrived or the parked entry: header in pdx / poff / pmeta, payload in pl
         d = pdx;
         b = poff;
         meta = pmeta;

@@ -45,7 +45,11 @@ def bounded(x, d):
     return (x * d) >> 32
 
 
-def mode_of(c, d, list_max=20, bits=320, inline_bits=None):
+def mode_of(c, d, list_max=22, bits=352, inline_bits=None):
+    """Payload mode of a slot (gw_internal.h): d < 65536 entries pack kp | c in
+    one word and carry 11 payload words (352 bits, lists of 22), others 10."""
+    if d >= 65536:
+        bits = bits - 32
     if c <= list_max and d < 65536:
         return "list"
     if d <= (inline_bits or bits):
@@ -66,12 +70,12 @@ def main():
     ap.add_argument("--seed", type=int, default=42)
     # what-if knobs (defaults = the built kernel): payload bits, list length,
     # filter buckets with / without an in-entry directory, in-entry directory limit
-    ap.add_argument("--payload-bits", type=int, default=320)
-    ap.add_argument("--list-max", type=int, default=20)
+    ap.add_argument("--payload-bits", type=int, default=352)
+    ap.add_argument("--list-max", type=int, default=22)
     ap.add_argument("--inline-bits", type=int, default=None,
                     help="inline bitsets up to this degree (default: --payload-bits)")
-    ap.add_argument("--filter-dir", type=int, default=160)
-    ap.add_argument("--filter-nodir", type=int, default=288)
+    ap.add_argument("--filter-dir", type=int, default=192)
+    ap.add_argument("--filter-nodir", type=int, default=320)
     ap.add_argument("--tail-list", type=int, default=0,
                     help="what-if: entries with c <= this also carry their commons as positions in N(u)")
     ap.add_argument("--pdir", type=int, default=8, help="directory blocks kept in the entry (0: none)")
