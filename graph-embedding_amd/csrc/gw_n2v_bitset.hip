@@ -20,19 +20,20 @@
 // Per edge slot s = (u -> v):
 //   bs_nbr[s] (64 B, one HBM sector): v, d = deg(v), offsets[v] (u32: this
 //            mode needs < 2^32 slots), meta (payload mode, Elias-Fano l and U,
-//            directory blocks), kp (position of u in N(v)), c, and a 40 B
-//            payload: the common positions (u16 list or Elias-Fano), the
-//            bitset itself (d <= 320), or for a region: w[0] = its 64 B block
-//            index, w[1..4] = the directory (u16 counts, 512 < d <= 4096),
-//            then a draw filter over u (w[5..9]: 160 buckets, or w[1..9]: 288
-//            when the entry holds no directory; bucket = u*F >> 32, bit set
-//            iff some u in the bucket lands on a common position), so most
-//            "other"-branch membership tests never read the region
-//   region   (d > 320, payload full) dir[ndir]  cumulative set bits before
-//                       each 512-bit block (d > 4096 only), then
+//            directory blocks), kp (position of u in N(v)) and c — one word
+//            kp | c << 16 when d < 65536 — and a 44 B payload (40 B otherwise):
+//            the common positions (u16 list or Elias-Fano), the bitset itself
+//            (d <= 352), or for a region: w[0] = its 64 B block index, w[1..4]
+//            = the directory (u16 counts, 512 < d <= 4096), then a draw filter
+//            over u (w[5..10]: 192 buckets, or w[1..10]: 320 when the entry
+//            holds no directory; bucket = u*F >> 32, bit set iff some u in the
+//            bucket lands on a common position), so most "other"-branch
+//            membership tests never read the region
+//   region   (payload full) dir[ndir]  cumulative set bits before each 512-bit
+//                       block (d > 4096 only), then
 //            bits[ceil(d/32)]  bit k = (N(v)[k] != u) && has_edge(N(v)[k], u)
 // The entry chosen by a step carries everything the next step needs, so a
-// step into a vertex of degree <= 320 touches ONE random sector (the entry);
+// step into a vertex of degree <= 352 touches ONE random sector (the entry);
 // region selects and unfiltered membership tests add one (1.34 per step on
 // R-MAT-20, vs ~7 for rejection sampling with binary-search probes).
 //
