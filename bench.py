@@ -230,25 +230,33 @@ def cpu_baseline_walks(csr, p, q, seed, L, walk0, seconds, max_walks=3_000_000):
                       f"oracle/oracle.c or_walks_scale (rejection sampler, same walk law), {dt:.1f} s"}
 
 
-def cpu_baseline_topsim(offs, nbrs, n, sample, step, seed, seconds, sources=None):
+def cpu_baseline_topsim(offs, nbrs, n, sample, step, seed, seconds, sources=None, topk=20):
     """Oracle restatement of TopSim_singleSample (Java-literal queue, OpenMP
-    over sources) on a bounded prefix of the same sources."""
+    over sources) plus the per-source top-k the GPU line also produces
+    (oracle.topsim_topk: one reused row per thread, no n-wide rows), on an
+    evenly strided sample of the same sources (R-MAT puts its hubs at low ids,
+    so a prefix would over-weight them)."""
     import numpy as np
     import oracle
     cores = cores_used()
     srcs = np.arange(n, dtype=np.int32) if sources is None else np.asarray(sources, np.int32)
+
+    def strided(k):
+        k = max(1, min(len(srcs), k))
+        return srcs[np.linspace(0, len(srcs) - 1, k).astype(np.int64)]
     ns = min(len(srcs), 256)
     t0 = time.perf_counter()
-    oracle.topsim(offs, nbrs, 0, sample, step, C=0.6, seed=seed, sources=srcs[:ns], nthreads=cores)
+    oracle.topsim_topk(offs, nbrs, 0, sample, step, topk, C=0.6, seed=seed, sources=strided(ns), nthreads=cores)
     dt = time.perf_counter() - t0
     ns2 = int(min(len(srcs), max(ns, ns * seconds / max(dt, 1e-3))))
     t0 = time.perf_counter()
-    _, st = oracle.topsim(offs, nbrs, 0, sample, step, C=0.6, seed=seed, sources=srcs[:ns2], nthreads=cores)
+    _, _, st = oracle.topsim_topk(offs, nbrs, 0, sample, step, topk, C=0.6, seed=seed, sources=strided(ns2),
+                                  nthreads=cores)
     dt = time.perf_counter() - t0
     return {"value": st["pair_updates"] / dt, "unit": "pair-updates/s", "cores": cores, "kind": "port",
-            "sample": f"the first {ns2} sources ({st['pair_updates']} pair-updates), oracle/oracle.c or_topsim "
-                      f"(TopSim_singleSample.java queue restated), {dt:.1f} s; the Java reference cannot run "
-                      "here (no JDK)"}
+            "sample": f"{ns2} of the {len(srcs)} sources, evenly strided ({st['pair_updates']} pair-updates), "
+                      f"oracle/oracle.c or_topsim_topk (TopSim_singleSample.java queue restated + top-{topk} per "
+                      f"row), {dt:.1f} s; the Java reference cannot run here (no JDK)"}
 
 
 def reference_cpu_fixture():
@@ -751,7 +759,7 @@ def run_topsim(R, args, name):
     cpu_ts = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu_ts = cpu_baseline_topsim(offs, nbrs, len(offs) - 1, sample, step, args.seed,
-                                     args.cpu_seconds if name != "p10m" else 15.0, sources=srcs)
+                                     args.cpu_seconds if name != "p10m" else 15.0, sources=srcs, topk=K)
     del keep
     return {
         "metric": "SimRank pair-updates/sec (TopSim_singleSample)", "value": upd / tel,

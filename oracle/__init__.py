@@ -52,6 +52,7 @@ def lib():
         L.or_walks_bitset.argtypes = [i64, v, v, v, d, d, u64, ci, i64, i64, ci, v, v, v, ci]
         L.or_topsim.argtypes = [i64, v, v, ci, ci, ci, d, u64, ci, i64, v, i64, v, v, ci]
         L.or_simrank_naive.argtypes = [i64, v, v, d, ci, v, ci]
+        L.or_topsim_topk.argtypes = [i64, v, v, ci, ci, ci, d, u64, v, i64, ci, v, v, v, ci]
         L.or_topsim_m.argtypes = [i64, v, v, ci, ci, ci, d, u64, ci, v, i64, v, v, v, v, ci]
         L.or_fcm_run.argtypes = [ci, i64, v, v, v, v]
         L.or_topsim_levels.argtypes = [i64, v, v, ci, ci, u64, v, v, i64, v, ci]
@@ -182,6 +183,23 @@ def topsim(offsets, nbrs, variant, sample, step, C=0.6, seed=0, sources=None, rn
                     int(nthreads))
     return rows, dict(extensions=int(st[0]), pair_updates=int(st[1]), max_frontier=int(st[2]),
                       walkers=int(st[3]))
+
+
+def topsim_topk(offsets, nbrs, variant, sample, step, topk, C=0.6, seed=0, sources=None, nthreads=0):
+    """Per-source top-k (score desc, id asc; padded with id -1 / score 0) of the
+    same TopSim rows as topsim(), without materialising n-wide rows per source
+    (oracle.c or_topsim_topk): the CPU comparator for large graphs."""
+    off = np.ascontiguousarray(offsets, np.int64)
+    nb = np.ascontiguousarray(nbrs, np.int32)
+    n = len(off) - 1
+    src = np.arange(n, dtype=np.int32) if sources is None else np.ascontiguousarray(sources, np.int32)
+    ids = np.empty((len(src), topk), np.int32)
+    sc = np.empty((len(src), topk), np.float64)
+    st = np.zeros(4, np.int64)
+    lib().or_topsim_topk(n, _p(off), _p(nb), int(variant), int(sample), int(step), float(C), int(seed),
+                         _p(src), len(src), int(topk), _p(ids), _p(sc), _p(st), int(nthreads))
+    return ids, sc, dict(extensions=int(st[0]), pair_updates=int(st[1]), max_frontier=int(st[2]),
+                         walkers=int(st[3]))
 
 
 def simrank_naive(offsets, nbrs, C, iters, nthreads=0):

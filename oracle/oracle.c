@@ -476,9 +476,26 @@ typedef struct {
   int64_t ext, upd, maxf, walkers;
 } tstats;
 
+/* touched-target list of one source (top-k mode): every increment is > 0, so
+   row[t] == 0 before an add means t enters the row for the first time */
+typedef struct {
+  int32_t* ids;
+  int64_t size, cap;
+} tlist;
+static void row_add(double* row, tlist* tl, int32_t t, double v) {
+  if (tl && row[t] == 0.0) {
+    if (tl->size == tl->cap) {
+      tl->cap = tl->cap ? 2 * tl->cap : 4096;
+      tl->ids = (int32_t*)realloc(tl->ids, sizeof(int32_t) * tl->cap);
+    }
+    tl->ids[tl->size++] = t;
+  }
+  row[t] += v;
+}
+
 static void topsim_one(const int64_t* off, const int32_t* nbrs, int variant, int SAMPLE, int STEP,
                        const double* cache, uint32_t k0, uint32_t k1, int rng, jrand* jr, int32_t src,
-                       double* row, pqueue* A, pqueue* B, tstats* st, fcm* map) {
+                       double* row, pqueue* A, pqueue* B, tstats* st, fcm* map, tlist* tl) {
   const int L = 2 * STEP;
   if (variant == 2) { /* SingleRandomWalk.walk :53-72 + computePathSim :81-92 */
     int32_t* path = (int32_t*)malloc(sizeof(int32_t) * (L + 1));
@@ -512,7 +529,7 @@ static void topsim_one(const int64_t* off, const int32_t* nbrs, int variant, int
           if (map)
             fcm_put(map, target, (float)incre); /* SingleRandomWalk_M.java:computePathSim */
           else
-            row[target] += incre;
+            row_add(row, tl, target, incre);
           st->upd++;
         }
       }
@@ -551,7 +568,7 @@ static void topsim_one(const int64_t* off, const int32_t* nbrs, int variant, int
               if (map) /* TopSim_singleSample_M.java:224-225 */
                 fcm_put(map, target, (float)((((mass[2 * i] * cache[i]) * dm) / dt) / (double)SAMPLE));
               else
-                row[target] += ((mass[2 * i] * cache[i]) * dm) / dt; /* :189 */
+                row_add(row, tl, target, ((mass[2 * i] * cache[i]) * dm) / dt); /* :189 */
               st->upd++;
             }
           }
@@ -632,7 +649,7 @@ void or_topsim(int64_t n, const int64_t* off, const int32_t* nbrs, int variant, 
     pqueue A = {0}, B = {0};
     tstats st = {0, 0, 0, 0};
     for (int64_t r = 0; r < nsrc; ++r)
-      topsim_one(off, nbrs, variant, sample, step, cache, k0, k1, 1, &jr, sources[r], rows + r * n, &A, &B, &st, NULL);
+      topsim_one(off, nbrs, variant, sample, step, cache, k0, k1, 1, &jr, sources[r], rows + r * n, &A, &B, &st, NULL, NULL);
     e = st.ext;
     u = st.upd;
     mf = st.maxf;
@@ -651,7 +668,7 @@ void or_topsim(int64_t n, const int64_t* off, const int32_t* nbrs, int variant, 
 #pragma omp for schedule(dynamic, 1)
 #endif
       for (int64_t r = 0; r < nsrc; ++r)
-        topsim_one(off, nbrs, variant, sample, step, cache, k0, k1, 0, NULL, sources[r], rows + r * n, &A, &B, &st, NULL);
+        topsim_one(off, nbrs, variant, sample, step, cache, k0, k1, 0, NULL, sources[r], rows + r * n, &A, &B, &st, NULL, NULL);
       e += st.ext;
       u += st.upd;
       w += st.walkers;
@@ -673,6 +690,85 @@ void or_topsim(int64_t n, const int64_t* off, const int32_t* nbrs, int variant, 
 /* FixedCacheMap(capacity) in the reference's order; per source the map is   */
 /* drained ascending (its iteration order): out_keys/out_vals[r*cap + i],   */
 /* out_size[r].                                                            */
+typedef struct {
+  double v;
+  int32_t id;
+} vid;
+static int vid_cmp(const void* a, const void* b) { /* score desc, id asc (Print.printByOrder order) */
+  const vid *x = (const vid*)a, *y = (const vid*)b;
+  if (x->v != y->v) return x->v > y->v ? -1 : 1;
+  return (x->id > y->id) - (x->id < y->id);
+}
+
+/* Per-source top-k of sim[source][*] (Print.printByOrder, Print.java:25-53):
+   the same walks and sums as or_topsim, with one reused dense row per thread
+   whose touched entries are ranked and re-zeroed (no n-wide memset per
+   source, so large graphs cost what the walks cost).  ids/scores[r*topk ..]:
+   score desc, id asc; rows with fewer than topk positive entries are padded
+   with id -1, score 0 (the GPU's convention). */
+void or_topsim_topk(int64_t n, const int64_t* off, const int32_t* nbrs, int variant, int sample, int step,
+                    double C, uint64_t seed, const int32_t* sources, int64_t nsrc, int topk, int32_t* ids,
+                    double* scores, int64_t* stats, int nthreads) {
+  double cache[32];
+  for (int i = 0; i < 32; ++i) cache[i] = 0.0;
+  for (int i = 1; i <= step && i < 32; ++i) cache[i] = pow(C, (double)i); /* :42-43 */
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32) ^ GW_TAG_TOPSIM;
+  int64_t e = 0, u = 0, mf = 0, w = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel reduction(+ : e, u, w) reduction(max : mf)
+#endif
+  {
+    pqueue A = {0}, B = {0};
+    tstats st = {0, 0, 0, 0};
+    tlist tl = {0};
+    double* row = (double*)calloc((size_t)n, sizeof(double));
+    vid* buf = NULL;
+    int64_t bcap = 0;
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+    for (int64_t r = 0; r < nsrc; ++r) {
+      tl.size = 0;
+      topsim_one(off, nbrs, variant, sample, step, cache, k0, k1, 0, NULL, sources[r], row, &A, &B, &st, NULL, &tl);
+      if (tl.size > bcap) {
+        bcap = tl.size;
+        buf = (vid*)realloc(buf, sizeof(vid) * bcap);
+      }
+      int64_t m = 0;
+      for (int64_t i = 0; i < tl.size; ++i) {
+        const int32_t t = tl.ids[i];
+        if (row[t] > 0.0) {
+          buf[m].v = row[t];
+          buf[m].id = t;
+          ++m;
+        }
+        row[t] = 0.0;
+      }
+      qsort(buf, (size_t)m, sizeof(vid), vid_cmp);
+      for (int k = 0; k < topk; ++k) {
+        ids[r * topk + k] = k < m ? buf[k].id : -1;
+        scores[r * topk + k] = k < m ? buf[k].v : 0.0;
+      }
+    }
+    e += st.ext;
+    u += st.upd;
+    w += st.walkers;
+    if (st.maxf > mf) mf = st.maxf;
+    free(A.cur); free(A.mass); free(A.walker);
+    free(B.cur); free(B.mass); free(B.walker);
+    free(tl.ids);
+    free(buf);
+    free(row);
+  }
+  if (stats) {
+    stats[0] = e;
+    stats[1] = u;
+    stats[2] = mf;
+    stats[3] = w;
+  }
+}
+
 void or_topsim_m(int64_t n, const int64_t* off, const int32_t* nbrs, int variant, int sample, int step,
                  double C, uint64_t seed, int capacity, const int32_t* sources, int64_t nsrc, int32_t* out_keys,
                  float* out_vals, int32_t* out_size, int64_t* stats, int nthreads) {
@@ -696,7 +792,7 @@ void or_topsim_m(int64_t n, const int64_t* off, const int32_t* nbrs, int variant
 #endif
     for (int64_t r = 0; r < nsrc; ++r) {
       fcm_clear(&m);
-      topsim_one(off, nbrs, variant, sample, step, cache, k0, k1, 0, NULL, sources[r], NULL, &A, &B, &st, &m);
+      topsim_one(off, nbrs, variant, sample, step, cache, k0, k1, 0, NULL, sources[r], NULL, &A, &B, &st, &m, NULL);
       out_size[r] = fcm_drain(&m, out_keys + r * (int64_t)capacity, out_vals + r * (int64_t)capacity);
     }
     e += st.ext;
