@@ -14,6 +14,7 @@
 // resident; the grid is 256 CUs x W workgroups (all resident, no tail).
 //
 //   calib_sweep [--quick] [--sizes MB,MB,..] [--rb 64,128] [--waves 5] [--dep 0,1] [--reps N]
+//               [--alloc default|contiguous]   (hipMalloc or hipExtMallocWithFlags(hipDeviceMallocContiguous))
 //
 // Output: one JSON object per line:
 //   {"rb":64,"dep":0,"waves":5,"table_mb":2048,"blocks_per_s":..,"bytes_per_s":..,"ms":..,"reads":..}
@@ -109,6 +110,7 @@ int main(int argc, char** argv) {
   std::vector<long long> waves = {4, 5, 6, 8};
   std::vector<long long> deps = {0, 1};
   int reps = 3, iters = 256;
+  int contiguous = 0;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--quick")) {
       sizes_mb = {2048, 8192};
@@ -124,6 +126,8 @@ int main(int argc, char** argv) {
       deps = parse_list(argv[++i]);
     } else if (!strcmp(argv[i], "--reps") && i + 1 < argc) {
       reps = atoi(argv[++i]);
+    } else if (!strcmp(argv[i], "--alloc") && i + 1 < argc) {
+      contiguous = !strcmp(argv[++i], "contiguous");
     } else if (!strcmp(argv[i], "--iters") && i + 1 < argc) {
       iters = atoi(argv[++i]);
     }
@@ -135,7 +139,10 @@ int main(int argc, char** argv) {
   const int cus = prop.multiProcessorCount;
   const size_t maxb = (size_t)maxmb << 20;
   uint4* buf;
-  CK(hipMalloc(&buf, maxb));
+  if (contiguous)
+    CK(hipExtMallocWithFlags((void**)&buf, maxb, hipDeviceMallocContiguous));
+  else
+    CK(hipMalloc(&buf, maxb));
   CK(hipMemset(buf, 0x5a, maxb));
   unsigned* out;
   CK(hipMalloc(&out, (size_t)cus * 8 * 256 * 4));
@@ -167,8 +174,9 @@ int main(int argc, char** argv) {
           }
           const double reads = (double)blocks * 256.0 * iters;
           printf("{\"rb\":%lld,\"dep\":%lld,\"waves\":%lld,\"table_mb\":%lld,\"blocks_per_s\":%.4g,"
-                 "\"bytes_per_s\":%.4g,\"ms\":%.4f,\"reads\":%.0f}\n",
-                 rb, dep, w, smb, reads / (best * 1e-3), reads * rb / (best * 1e-3), best, reads);
+                 "\"bytes_per_s\":%.4g,\"ms\":%.4f,\"reads\":%.0f,\"alloc\":\"%s\"}\n",
+                 rb, dep, w, smb, reads / (best * 1e-3), reads * rb / (best * 1e-3), best, reads,
+                 contiguous ? "contiguous" : "default");
           fflush(stdout);
         }
   CK(hipFree(buf));
