@@ -244,15 +244,17 @@ def cpu_baseline_topsim(offs, nbrs, n, sample, step, seed, seconds, sources=None
     def strided(k):
         k = max(1, min(len(srcs), k))
         return srcs[np.linspace(0, len(srcs) - 1, k).astype(np.int64)]
-    ns = min(len(srcs), 256)
-    t0 = time.perf_counter()
-    oracle.topsim_topk(offs, nbrs, 0, sample, step, topk, C=0.6, seed=seed, sources=strided(ns), nthreads=cores)
-    dt = time.perf_counter() - t0
-    ns2 = int(min(len(srcs), max(ns, ns * seconds / max(dt, 1e-3))))
-    t0 = time.perf_counter()
-    _, _, st = oracle.topsim_topk(offs, nbrs, 0, sample, step, topk, C=0.6, seed=seed, sources=strided(ns2),
-                                  nthreads=cores)
-    dt = time.perf_counter() - t0
+    # grow the sample until it takes about `seconds` (the first calls also pay the
+    # per-thread row allocation, so one extrapolation undershoots on large graphs)
+    ns2 = min(len(srcs), 256)
+    for _ in range(4):
+        t0 = time.perf_counter()
+        _, _, st = oracle.topsim_topk(offs, nbrs, 0, sample, step, topk, C=0.6, seed=seed, sources=strided(ns2),
+                                      nthreads=cores)
+        dt = time.perf_counter() - t0
+        if dt >= 0.5 * seconds or ns2 >= len(srcs):
+            break
+        ns2 = int(min(len(srcs), max(2 * ns2, ns2 * seconds / max(dt, 1e-3))))
     return {"value": st["pair_updates"] / dt, "unit": "pair-updates/s", "cores": cores, "kind": "port",
             "sample": f"{ns2} of the {len(srcs)} sources, evenly strided ({st['pair_updates']} pair-updates), "
                       f"oracle/oracle.c or_topsim_topk (TopSim_singleSample.java queue restated + top-{topk} per "
