@@ -86,7 +86,7 @@ typedef void (*KFn)(const uint4*, unsigned long long, int, unsigned*);
 static KFn pick(int rb, int dep) {
 #define P(R)                                 \
   if (rb == R) return dep ? k_coop<R, 1> : k_coop<R, 0>;
-  P(32) P(64) P(128) P(256)
+  P(16) P(32) P(64) P(128) P(256)
 #undef P
   return nullptr;
 }

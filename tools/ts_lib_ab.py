@@ -1,0 +1,120 @@
+"""In-process A/B of TopSim library variants (config 5 P10M and the lshrank graphs).
+
+Every library (ctypes, RTLD_LOCAL) builds its own graph; launches are
+interleaved A B B A ... with HIP events on one stream, so each variant sees
+the same box state.  Also reports the counters and the top-k agreement of
+every variant with the first (fp64 atomics make the last bits order-dependent).
+
+    python tools/ts_lib_ab.py main abl/ts_flat.so [--graphs p10m,blog,arxiv] [--reps 4]
+("main" = the in-tree gwamd/libgraphwalk.so)
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "graph-embedding_amd"))
+
+GRAPHS = {"blog": ("blog.txt", 10313, ",", 10000, 5, 20),
+          "arxiv": ("arxiv_author_pub.txt", 38741, "\t", 10000, 5, 20),
+          "moreno": ("moreno_crime_crime.txt", 1380, "\t", 10000, 5, 20)}
+
+
+def load(path, C):
+    L = ctypes.CDLL(path)
+    for name, (res, args) in C.SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--graphs", default="p10m,blog,arxiv")
+    ap.add_argument("--reps", type=int, default=4)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    from gwamd import _lib as C
+    paths = [os.path.join(ROOT, "graph-embedding_amd", "gwamd", "libgraphwalk.so") if x == "main"
+             else os.path.join(ROOT, x) for x in a.libs]
+    libs = [load(p, C) for p in paths]
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.current_stream(dev)
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    for gname in a.graphs.split(","):
+        hs = []
+        for L in libs:
+            h = ctypes.c_void_p()
+            t0 = time.perf_counter()
+            if gname == "p10m":
+                rc = L.gw_graph_rmat_java(10_000_000, 100_000_000, 0.57, 0.19, 0.19, 42, ctypes.byref(h))
+                K, sample, step = 100, 1000, 3
+            else:
+                f, V, sep, sample, step, K = GRAPHS[gname]
+                rc = L.gw_graph_load_edgelist(os.path.join(ROOT, "tests", "golden", "data", f).encode(),
+                                              sep.encode(), C.SEM_JAVA_MULTI, 0, 0, V, ctypes.byref(h))
+            if rc != 0 or L.gw_graph_to_device(h, 0) != 0:
+                raise SystemExit(f"graph {gname}: rc {rc}")
+            hs.append(h)
+            print(f"[{gname}] graph built in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+        inf = C.GraphInfo()
+        libs[0].gw_graph_info(hs[0], ctypes.byref(inf))
+        n = int(inf.n)
+        offs = np.empty(n + 1, np.int64)
+        # sources: every vertex with an edge (degree from the exported CSR)
+        nnz = int(inf.nnz)
+        nb = np.empty(max(nnz, 1), np.int32)
+        libs[0].gw_graph_export_csr(hs[0], offs.ctypes.data, nb.ctypes.data, None, None, None)
+        srcs = np.nonzero(np.diff(offs) > 0)[0].astype(np.int32)
+        del nb
+        src = torch.as_tensor(srcs, device=dev)
+        ns = len(srcs)
+        outs = [(torch.empty((ns, K), dtype=torch.int32, device=dev),
+                 torch.empty((ns, K), dtype=torch.float64, device=dev)) for _ in libs]
+        st = torch.zeros(4, dtype=torch.int64, device=dev)
+        times = [[] for _ in libs]
+        stats = [None] * len(libs)
+
+        def run(k):
+            st.zero_()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            rc = libs[k].gw_topsim(hs[k], C.TOPSIM_SINGLE_SAMPLE, sample, step, 0.6, 42, C.ptr(src), ns, K,
+                                   C.ptr(outs[k][0]), C.ptr(outs[k][1]), C.ptr(st), sh)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            if rc != 0:
+                raise SystemExit(libs[k].gw_last_error(hs[k]).decode())
+            return e0.elapsed_time(e1)
+        for k in range(len(libs)):
+            run(k)  # warm-up, workspace
+        for r in range(a.reps):
+            order = list(range(len(libs))) if r % 2 == 0 else list(reversed(range(len(libs))))
+            for k in order:
+                times[k].append(run(k))
+                stats[k] = [int(x) for x in st.cpu().tolist()]
+            print(f"[{gname}] rep {r}: " + " ".join(f"{t[-1]:.2f}" for t in times), file=sys.stderr, flush=True)
+        base = statistics.median(times[0])
+        for k, name in enumerate(a.libs):
+            ids_eq = float((outs[k][0] == outs[0][0]).float().mean().item())
+            rel = float(((outs[k][1] - outs[0][1]).abs() / outs[0][1].abs().clamp_min(1e-300)).max().item())
+            med = statistics.median(times[k])
+            print(json.dumps({"graph": gname, "lib": name, "median_ms": round(med, 3),
+                              "ms": [round(x, 3) for x in times[k]], "vs_first": round(med / base, 4),
+                              "stats": stats[k], "ids_equal_frac_vs_first": ids_eq,
+                              "max_rel_score_diff_vs_first": rel}), flush=True)
+        for L, h in zip(libs, hs):
+            L.gw_graph_free(h)
+        del outs
+        torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()
