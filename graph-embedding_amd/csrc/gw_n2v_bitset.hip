@@ -644,6 +644,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
     uint32_t sw = 0u, sbit = 0u;
     uint64_t sec = 0ull;  // 64 B sector this lane fetches: its next entry or a region block
     bool isblk = false;
+    bool virt = false;    // return whose entry is already known (no fetch)
     if (active) {
       const uint32_t mode = meta & 3u;
       const int efl = (int)((meta >> 2) & 31u);
@@ -763,7 +764,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
           }
         } else if (op == 2) {
           if (mode == BS_LIST) {
-            common = list_has(pl, (uint32_t)k);
+            common = c != 0u && list_has(pl, (uint32_t)k);  // c == 0: pl may hold the return stash
           } else if (mode == BS_INLINE) {
             common = win & 1u;
           } else if (mode == BS_EF) {
@@ -785,8 +786,15 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
         isblk = true;
       }
       if (acc) {
-        slot = b + (uint32_t)k;
-        sec = (uint64_t)(ents + (uint64_t)slot * 4u);
+        if ((meta >> 31) && k == (int64_t)kp) {
+          // return over an edge with no common neighbours: the entry of the
+          // reverse slot (cur -> prev) is {prev, its degree and row, kp = the
+          // index drawn at prev, c = 0, empty list}, all kept in pl[0..3]
+          virt = true;
+        } else {
+          slot = b + (uint32_t)k;
+          sec = (uint64_t)(ents + (uint64_t)slot * 4u);
+        }
       }
     }
     // cooperative sector load (entries and region blocks alike): all four
@@ -824,19 +832,41 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
       ph = 3;
     }
     if (slot != 0xFFFFFFFFu) {
+      const uint32_t ou = (uint32_t)cur, od = d, ob = b, ok = slot - b;
       cur = (int32_t)E[0];
       d = E[1];
       b = E[2];
       meta = E[3];
       unpack_entry(E, &kp, &c, pl);
+      if (c == 0u && d < GW_BS_PACK_D && od < GW_BS_PACK_D) {
+        // empty list: its payload words keep the row we came from (a later
+        // return needs no fetch); bit 31 of meta marks the stash (list mode)
+        pl[0] = ou;
+        pl[1] = od;
+        pl[2] = ob;
+        pl[3] = ok;
+        meta = 0x80000000u;
+      }
     }
-    if (slot != 0xFFFFFFFFu) {
+    if (virt) {  // swap the current row and the stash: the walker is back at prev
+      const uint32_t tc = (uint32_t)cur, td = d, tb = b, tk = kp;
+      cur = (int32_t)pl[0];
+      d = pl[1];
+      b = pl[2];
+      kp = pl[3];
+      pl[0] = tc;
+      pl[1] = td;
+      pl[2] = tb;
+      pl[3] = tk;
+    }
+    const bool moved = slot != 0xFFFFFFFFu || virt;
+    if (moved) {
       my_trials += trial;
       trial = 0;
     }
     bool ready = false;  // this lane completed 16 staged positions (flen-15 .. flen)
     int flen = 0;
-    if (slot != 0xFFFFFFFFu) {
+    if (moved) {
       stage[64 * (len & (kStage - 1))] = cur;
       ready = (len & (kStage - 1)) == kStage - 1;
       flen = len;
