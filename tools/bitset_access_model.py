@@ -134,6 +134,8 @@ def main():
                     r = u[0] * 2.3283064365386963e-10 * Z
                     if r < ap_:
                         add("branch_return")
+                        if c == 0 and d < 65536 and len(prow) < 65536:
+                            add("entry_elided_return")  # return elision: the reverse entry is the stash
                         if last_ret:
                             add("return_after_return")  # entry = the one read two steps earlier
                         last_ret = True
@@ -169,13 +171,16 @@ def main():
         res[k + "_per_step"] = v / steps
     extra = sum(v for k, v in cnt.items() if k.startswith("sectors_")) / steps
     res["extra_region_sectors_per_step"] = extra
-    res["model_read_sectors_per_step"] = 1.0 + extra + 2.0 / L  # + entry; + walk starts (order, offsets)
+    elided = cnt.get("entry_elided_return", 0) / steps
+    res["model_read_sectors_per_step"] = 1.0 - elided + extra + 2.0 / L  # + entry (less elided returns); + walk starts
     res["iterations_per_walk_mean"] = float(iters.mean())
     res["wave_lane_occupancy"] = occupancy
     try:
         pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))
-        e = pmc[f"n2v_rmat{a.scale}_p{a.p}_q{a.q}_L80_r10_bitset"]
-        res["measured_fabric_read_requests_per_step"] = e["fabric_read_requests_per_launch"] / e["walk_steps_per_launch"]
+        e = pmc.get(f"n2v_rmat{a.scale}_ef16_p{a.p}_q{a.q}_L80_r10_bitset") or pmc[f"n2v_rmat{a.scale}_p{a.p}_q{a.q}_L80_r10_bitset"]
+        units = e.get("units_per_launch") or e["walk_steps_per_launch"]
+        res["measured_fabric_read_requests_per_step"] = e["fabric_read_requests_per_launch"] / units
+        res["measured_lib_sha256"] = e.get("lib_sha256")
     except Exception:
         pass
     print(json.dumps(res, indent=1))
