@@ -83,8 +83,18 @@ const char* gw_strerror(int code) {
 }
 
 gw_device_guard::gw_device_guard(int dev) {
+  if (dev < 0) return;  // host-only handle: nothing to select
   int cur = -1;
-  if (dev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+  if (hipGetDevice(&cur) != hipSuccess) {
+    ok = false;
+    return;
+  }
+  if (cur == dev) return;
+  if (hipSetDevice(dev) != hipSuccess) {
+    ok = false;
+    return;
+  }
+  prev = cur;
 }
 gw_device_guard::~gw_device_guard() {
   if (prev >= 0) (void)hipSetDevice(prev);
@@ -247,7 +257,7 @@ int gw_graph_export_csr(const gw_graph* g, int64_t* offsets, int32_t* nbrs, doub
 int gw_graph_free(gw_graph* g) {
   if (!g) return GW_OK;
   {
-    gw_device_guard dg(g->device);
+    gw_device_guard dg(g->device);  // best effort: release even if the switch failed
     gw_dev_release(g);
   }
   delete g;
@@ -256,13 +266,13 @@ int gw_graph_free(gw_graph* g) {
 
 int gw_graph_to_device(gw_graph* g, int device) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(device);
+  GW_GUARD_DEVICE(g, device);
   return ret(g, gw_dev_upload(g, device));
 }
 
 int gw_n2v_prepare(gw_graph* g, double p, double q, int mode) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);
+  GW_GUARD_DEVICE(g, g->device);
   if (!(p > 0) || !(q > 0)) return ret(g, gw_fail(g, GW_ERR_ZERODIV, "p and q must be > 0 (node2vec.py:70-76 divides by them)"));
   if (mode != GW_N2V_REPLAY && mode != GW_N2V_REJECTION && mode != GW_N2V_BITSET)
     return ret(g, gw_fail(g, GW_ERR_INVALID, "unknown mode %d", mode));
@@ -287,7 +297,7 @@ int gw_n2v_export_alias(const gw_graph* g_, int32_t* node_J, double* node_q, int
 int gw_alias_setup(int device, const double* probs, int64_t K, int64_t* J, double* q) {
   if (K < 0 || (K > 0 && (!probs || !J || !q))) return gw_fail(nullptr, GW_ERR_INVALID, "bad arrays");
   std::string err;
-  gw_device_guard dg(device);
+  GW_GUARD_DEVICE(nullptr, device);
   int rc = gw_dev_alias_setup(device, probs, K, J, q, &err);
   if (rc != GW_OK) return gw_fail(nullptr, rc, "%s", err.c_str());
   return GW_OK;
@@ -297,7 +307,7 @@ int gw_n2v_walks_replay(gw_graph* g, int walk_len, int64_t nwalks, const int32_t
                         const double* uniforms, int64_t n_uniforms, int32_t* out_walks,
                         int32_t* out_len, int64_t* uniforms_used) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);
+  GW_GUARD_DEVICE(g, g->device);
   if (!g->n2v_prepared || g->n2v_mode != GW_N2V_REPLAY)
     return ret(g, gw_fail(g, GW_ERR_STATE, "call gw_n2v_prepare(..., GW_N2V_REPLAY) first"));
   if (walk_len < 1 || nwalks < 0 || (nwalks > 0 && (!starts || !out_walks || !out_len)) ||
@@ -317,7 +327,7 @@ int gw_n2v_walks(gw_graph* g, int walk_len, uint64_t seed, int64_t walk_begin, i
                  int shuffle, int32_t* out_walks_dev, int32_t* out_len_dev, uint64_t* counters_dev,
                  void* stream) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);
+  GW_GUARD_DEVICE(g, g->device);
   if (!g->n2v_prepared) return ret(g, gw_fail(g, GW_ERR_STATE, "call gw_n2v_prepare first"));
   if (walk_len < 1 || walk_begin < 0 || walk_count < 0 || (walk_count > 0 && !out_walks_dev))
     return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
@@ -328,7 +338,7 @@ int gw_n2v_walks(gw_graph* g, int walk_len, uint64_t seed, int64_t walk_begin, i
 
 int gw_topsim_prepare(gw_graph* g, int variant, int sample, int step, int topk) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);
+  GW_GUARD_DEVICE(g, g->device);
   return ret(g, gw_dev_topsim_prepare(g, variant, sample, step, topk));
 }
 
@@ -336,7 +346,7 @@ int gw_topsim(gw_graph* g, int variant, int sample, int step, double C, uint64_t
               const int32_t* sources_dev, int64_t nsrc, int topk, int32_t* out_ids_dev,
               double* out_scores_dev, int64_t* stats_dev, void* stream) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);
+  GW_GUARD_DEVICE(g, g->device);
   if (g->device < 0) return ret(g, gw_fail(g, GW_ERR_STATE, "graph is not on a device"));
   if (nsrc < 0 || (nsrc > 0 && (!sources_dev || !out_ids_dev || !out_scores_dev)) || topk < 0)
     return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
@@ -348,7 +358,7 @@ int gw_topsim_dense(gw_graph* g, int variant, int sample, int step, double C, ui
                     const int32_t* sources_dev, int64_t nsrc, double* out_rows_dev,
                     int64_t* stats_dev, void* stream) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);
+  GW_GUARD_DEVICE(g, g->device);
   if (g->device < 0) return ret(g, gw_fail(g, GW_ERR_STATE, "graph is not on a device"));
   if (nsrc < 0 || (nsrc > 0 && (!sources_dev || !out_rows_dev)))
     return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
@@ -356,11 +366,34 @@ int gw_topsim_dense(gw_graph* g, int variant, int sample, int step, double C, ui
                               out_rows_dev, stats_dev, stream));
 }
 
+int gw_topsim_sparse(gw_graph* g, int variant, int sample, int step, double C, uint64_t seed,
+                     const int32_t* sources_dev, int64_t nsrc, int64_t capacity, int64_t* row_begin_dev,
+                     int32_t* row_len_dev, int32_t* out_ids_dev, double* out_scores_dev, int64_t* used_dev,
+                     int64_t* stats_dev, void* stream) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  GW_GUARD_DEVICE(g, g->device);
+  if (g->device < 0) return ret(g, gw_fail(g, GW_ERR_STATE, "graph is not on a device"));
+  if (nsrc < 0 || capacity < 0 || !used_dev ||
+      (nsrc > 0 && (!sources_dev || !row_begin_dev || !row_len_dev || (capacity > 0 && (!out_ids_dev || !out_scores_dev)))))
+    return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
+  if (hipMemsetAsync(used_dev, 0, sizeof(int64_t), (hipStream_t)stream) != hipSuccess)
+    return ret(g, gw_fail(g, GW_ERR_DEVICE, "hipMemsetAsync(used_dev) failed"));
+  gw_ts_sparse sp;
+  sp.cap = capacity;
+  sp.begin = row_begin_dev;
+  sp.len = row_len_dev;
+  sp.ids = out_ids_dev;
+  sp.scores = out_scores_dev;
+  sp.cursor = reinterpret_cast<unsigned long long*>(used_dev);
+  return ret(g, gw_dev_topsim(g, variant, sample, step, C, seed, sources_dev, nsrc, 0, nullptr, nullptr, nullptr,
+                              stats_dev, stream, &sp));
+}
+
 int gw_topsim_m(gw_graph* g, int variant, int capacity, int sample, int step, double C, uint64_t seed,
                 const int32_t* sources_dev, int64_t nsrc, int32_t* out_keys_dev, float* out_vals_dev,
                 int32_t* out_size_dev, int64_t* stats_dev, void* stream) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);
+  GW_GUARD_DEVICE(g, g->device);
   if (g->device < 0) return ret(g, gw_fail(g, GW_ERR_STATE, "graph is not on a device"));
   if (nsrc < 0 || capacity < 1 || (nsrc > 0 && (!sources_dev || !out_keys_dev || !out_vals_dev || !out_size_dev)))
     return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
@@ -370,7 +403,7 @@ int gw_topsim_m(gw_graph* g, int variant, int capacity, int sample, int step, do
 
 int gw_topsim_double(gw_graph* g, int sample, int step, double C, uint64_t seed, double* sim_dev, void* stream) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);
+  GW_GUARD_DEVICE(g, g->device);
   if (g->n > 0 && !sim_dev) return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
   return ret(g, gw_dev_topsim_double(g, sample, step, C, seed, sim_dev, stream));
 }
@@ -378,21 +411,21 @@ int gw_topsim_double(gw_graph* g, int sample, int step, double C, uint64_t seed,
 int gw_topsim_dev(gw_graph* g, int sample, int step, int topK, int singleStep, double C, uint64_t seed,
                   const int32_t* cand_dev, double* sim_dev, void* stream) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);
+  GW_GUARD_DEVICE(g, g->device);
   if (g->n > 0 && (!sim_dev || (topK > 0 && !cand_dev))) return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
   return ret(g, gw_dev_topsim_dev(g, sample, step, topK, singleStep, C, seed, cand_dev, sim_dev, stream));
 }
 
 int gw_double_random_walk(gw_graph* g, int sample, int step, double C, uint64_t seed, double* sim_dev, void* stream) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);
+  GW_GUARD_DEVICE(g, g->device);
   if (g->n > 0 && !sim_dev) return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
   return ret(g, gw_dev_double_random_walk(g, sample, step, C, seed, sim_dev, stream));
 }
 
 int gw_simrank_naive(gw_graph* g, double C, int iters, double* sim_dev, void* stream) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);
+  GW_GUARD_DEVICE(g, g->device);
   if (g->device < 0) return ret(g, gw_fail(g, GW_ERR_STATE, "graph is not on a device"));
   if (g->directed) return ret(g, gw_fail(g, GW_ERR_UNSUPPORTED, "naive SimRank needs an undirected graph"));
   if (iters < 0 || (g->n > 0 && !sim_dev)) return ret(g, gw_fail(g, GW_ERR_INVALID, "bad arguments"));
@@ -426,6 +459,22 @@ int gw_write_sim_text_topk(const char* path, const int32_t* ids, const double* s
     return gw_fail(nullptr, GW_ERR_INVALID, "bad arguments");
   std::string err;
   int rc = gw_write_sim_topk_impl(path, ids, scores, row_ids, nrows, topk, sep ? sep : ",", decimals, &err);
+  if (rc != GW_OK) return gw_fail(nullptr, rc, "%s", err.c_str());
+  return GW_OK;
+}
+
+int gw_write_sim_text_sparse(const char* path, const int64_t* row_begin, const int32_t* row_len, const int32_t* ids,
+                             const double* scores, const int32_t* row_ids, int64_t nrows, int64_t n, int topk,
+                             const char* sep, int decimals) {
+  if (!path || n < 0 || topk < 0 || decimals < 0 || decimals > 30 || nrows < 0 ||
+      (nrows > 0 && (!row_begin || !row_len)))
+    return gw_fail(nullptr, GW_ERR_INVALID, "bad arguments");
+  for (int64_t r = 0; r < nrows; ++r)
+    if (row_len[r] > 0 && (!ids || !scores || row_begin[r] < 0))
+      return gw_fail(nullptr, GW_ERR_INVALID, "bad arguments");
+  std::string err;
+  int rc = gw_write_sim_sparse_impl(path, row_begin, row_len, ids, scores, row_ids, nrows, n, topk, sep ? sep : ",",
+                                    decimals, false, &err);
   if (rc != GW_OK) return gw_fail(nullptr, rc, "%s", err.c_str());
   return GW_OK;
 }

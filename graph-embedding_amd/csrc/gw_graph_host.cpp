@@ -846,6 +846,92 @@ int gw_write_sim_topk_impl(const char* path, const int32_t* ids, const double* s
   return rc;
 }
 
+// Print.printByOrder (Print.java:25-53) from sparse rows: row r lists its
+// nonzero entries (any order); every other column is 0.0.  FixedMaxPQ(topk)
+// is offered (i, sim[v][i]) for i = 0..n-1 (FixedMaxPQ.java:30-39).  The
+// first min(topk, n) offers fill the heap whatever their value (zeros
+// included); after that an offer enters only when the heap minimum compares
+// below it, which a 0.0 never does (scores are >= +0.0), so only the listed
+// nonzero entries past the fill need replaying, in id order.  The heap array
+// is then stably sorted in reverse (sortedElement(), FixedMaxPQ.java:72-76):
+// byte-identical to the dense writer on the same rows.
+int gw_sparse_rows_text(const int64_t* begin, const int32_t* len, const int32_t* ids, const double* scores,
+                        const int32_t* row_ids, int64_t nrows, int64_t n, int topk, const std::string& sep,
+                        int decimals, std::vector<std::string>* o, std::vector<std::string>* os, std::string* err) {
+  o->assign(nrows, std::string());
+  os->assign(nrows, std::string());
+  int bad = 0;
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t r = 0; r < nrows; ++r) {
+    std::vector<JPair> ent;
+    const int32_t m = len[r];
+    if (m < 0) {
+      bad = 1;
+      continue;
+    }
+    ent.reserve((size_t)m);
+    for (int32_t t = 0; t < m; ++t) ent.push_back(JPair{ids[begin[r] + t], scores[begin[r] + t]});
+    std::sort(ent.begin(), ent.end(), [](const JPair& a, const JPair& b) { return a.key < b.key; });
+    bool ok = true;
+    for (size_t t = 0; t < ent.size(); ++t)
+      if (ent[t].key < 0 || ent[t].key >= n || (t > 0 && ent[t].key == ent[t - 1].key) || !(ent[t].value > 0.0))
+        ok = false;
+    if (!ok) {
+      bad = 2;
+      continue;
+    }
+    JavaPQ pq;
+    const int64_t fill = std::min<int64_t>(topk, n);
+    pq.q.reserve((size_t)fill + 1);
+    size_t p = 0;
+    for (int64_t i = 0; i < fill; ++i) {
+      double v = 0.0;
+      if (p < ent.size() && ent[p].key == i) v = ent[p++].value;
+      pq.offer(JPair{(int32_t)i, v});
+    }
+    for (; p < ent.size() && fill > 0; ++p) {
+      if (JavaPQ::cmp(pq.q[0], ent[p]) < 0) {
+        pq.poll();
+        pq.offer(ent[p]);
+      }
+    }
+    std::vector<JPair> sorted(pq.q);
+    std::stable_sort(sorted.begin(), sorted.end(), [](const JPair& a, const JPair& b) { return JavaPQ::cmp(a, b) > 0; });
+    emit_row((*o)[r], (*os)[r], row_ids ? row_ids[r] : r, sorted, sep, decimals);
+  }
+  if (bad) {
+    *err = bad == 1 ? "a sparse row has length -1 (it did not fit the device output)"
+                    : "sparse row entries must be distinct ids in [0, n) with scores > 0";
+    return bad == 1 ? GW_ERR_INVALID : GW_ERR_RANGE;
+  }
+  return GW_OK;
+}
+
+int gw_write_sim_sparse_impl(const char* path, const int64_t* begin, const int32_t* len, const int32_t* ids,
+                             const double* scores, const int32_t* row_ids, int64_t nrows, int64_t n, int topk,
+                             const std::string& sep, int decimals, bool append, std::string* err) {
+  std::vector<std::string> o, os;
+  int rc = gw_sparse_rows_text(begin, len, ids, scores, row_ids, nrows, n, topk, sep, decimals, &o, &os, err);
+  if (rc != GW_OK) return rc;
+  std::string p2 = std::string(path) + ".sim.txt";
+  FILE* f1 = fopen(path, append ? "ab" : "wb");
+  FILE* f2 = fopen(p2.c_str(), append ? "ab" : "wb");
+  if (!f1 || !f2) {
+    if (f1) fclose(f1);
+    if (f2) fclose(f2);
+    *err = std::string("cannot open '") + path + "'";
+    return GW_ERR_IO;
+  }
+  for (int64_t r = 0; r < nrows; ++r) {
+    if (fwrite(o[r].data(), 1, o[r].size(), f1) != o[r].size()) rc = GW_ERR_IO;
+    if (fwrite(os[r].data(), 1, os[r].size(), f2) != os[r].size()) rc = GW_ERR_IO;
+  }
+  if (fclose(f1) != 0) rc = GW_ERR_IO;
+  if (fclose(f2) != 0) rc = GW_ERR_IO;
+  if (rc != GW_OK) *err = "write failed";
+  return rc;
+}
+
 // Print.printByOrder(FixedCacheMap[] sim, outPath, topk) (Print.java:94-124):
 // each row iterates its map ascending and prints the last `topk` entries,
 // "%.6f" of the float value (Formatter widens the float to double).

@@ -122,6 +122,18 @@ struct gw_topsim_ws {
   int* error_flag = nullptr;      // capacity overflow
 };
 
+// TopSim sparse rows (gw_topsim_sparse): per source r, row_len[r] nonzero
+// (id, score) entries at ids/scores[begin[r] ..], packed at offsets claimed
+// from *cursor (a row past `cap` gets begin = len = -1); on when cursor != nullptr
+struct gw_ts_sparse {
+  int64_t cap = 0;
+  int64_t* begin = nullptr;
+  int32_t* len = nullptr;
+  int32_t* ids = nullptr;
+  double* scores = nullptr;
+  unsigned long long* cursor = nullptr;
+};
+
 struct gw_graph {
   // host CSR
   int semantics = 0;
@@ -161,11 +173,23 @@ struct gw_graph {
 // current device and a NULL stream launches on the graph's own device.
 struct gw_device_guard {
   int prev = -1;
+  bool ok = true;  // false: the graph's device could not be selected (the call must fail)
   explicit gw_device_guard(int dev);
   ~gw_device_guard();
   gw_device_guard(const gw_device_guard&) = delete;
   gw_device_guard& operator=(const gw_device_guard&) = delete;
 };
+
+// every device-touching entry point: select the graph's device or fail with
+// GW_ERR_DEVICE (never run silently on the caller's current device)
+#define GW_GUARD_DEVICE(g, dev)                                                              \
+  gw_device_guard gw_dg_(dev);                                                               \
+  if (!gw_dg_.ok) return gw_fail((g), GW_ERR_DEVICE, "cannot select HIP device %d", (int)(dev))
+
+// Java-exact Print.printByOrder from sparse rows (gw_graph_host.cpp)
+int gw_write_sim_sparse_impl(const char* path, const int64_t* begin, const int32_t* len, const int32_t* ids,
+                             const double* scores, const int32_t* row_ids, int64_t nrows, int64_t n, int topk,
+                             const std::string& sep, int decimals, bool append, std::string* err);
 
 // error helpers (gw_capi.cpp)
 int gw_fail(gw_graph* g, int code, const char* fmt, ...);
@@ -214,4 +238,5 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step,
 int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C,
                   uint64_t seed, const int32_t* sources_dev, int64_t nsrc,
                   int topk, int32_t* out_ids_dev, double* out_scores_dev,
-                  double* out_rows_dev, int64_t* stats_dev, void* stream);
+                  double* out_rows_dev, int64_t* stats_dev, void* stream,
+                  const gw_ts_sparse* sparse = nullptr);

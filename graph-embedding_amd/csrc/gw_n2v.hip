@@ -929,7 +929,7 @@ extern "C" int gw_n2v_export_alias(const gw_graph* gc, int32_t* node_J, double* 
                                    int64_t* edge_off, int32_t* edge_J, double* edge_q) {
   gw_graph* g = const_cast<gw_graph*>(gc);
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);  // restores the caller's current device on return
+  GW_GUARD_DEVICE(g, g->device);  // restores the caller's current device on return
   if (!g->n2v_prepared) return gw_fail(g, GW_ERR_STATE, "call gw_n2v_prepare first");
   GW_HIP_TRY(hipSetDevice(g->device));
   const gw_dev_graph& d = g->d;
@@ -952,7 +952,7 @@ extern "C" int gw_n2v_walks_host(gw_graph* g, int walk_len, uint64_t seed, int64
                                  int64_t walk_count, int shuffle, int32_t* out_walks, int32_t* out_len,
                                  uint64_t* counters) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);  // restores the caller's current device on return
+  GW_GUARD_DEVICE(g, g->device);  // restores the caller's current device on return
   if (!g->n2v_prepared) return gw_fail(g, GW_ERR_STATE, "call gw_n2v_prepare first");
   if (walk_len < 1 || walk_begin < 0 || walk_count < 0 || (walk_count > 0 && !out_walks))
     return gw_fail(g, GW_ERR_INVALID, "bad arguments");

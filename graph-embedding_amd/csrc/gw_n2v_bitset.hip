@@ -138,6 +138,15 @@ __device__ __forceinline__ int bs_mode(uint32_t c, uint32_t d) {
   return gw_bs_is_list(c, d) ? BS_LIST : gw_bs_is_inline(d) ? BS_INLINE : gw_bs_is_ef(c, d) ? BS_EF : BS_REGION;
 }
 
+// Return elision (k_walk_bitset): an entry E(u -> x) with c = 0 lets the walk
+// keep E(x -> u) in its empty payload words — valid only when c(x -> u) = 0
+// too.  The two common sets differ only by the origin (x's self-loop counts
+// in c(u -> x), u's in c(x -> u)), so the builder marks a c = 0 list entry
+// whose u has no self-loop with meta == kMetaStashOk; after the walk has
+// written its stash, meta == kMetaStash.
+constexpr uint32_t kMetaStashOk = 0x40000000u;
+constexpr uint32_t kMetaStash = 0x80000000u;
+
 // per-entry constants of the step kernel (no divisions per step):
 // mode | Elias-Fano l << 2 | U << 7 | directory blocks before the bits << 16
 __device__ __forceinline__ uint32_t bs_meta(uint32_t c, uint32_t d) {
@@ -149,6 +158,12 @@ __device__ __forceinline__ uint32_t bs_meta(uint32_t c, uint32_t d) {
   }
   const uint32_t bblk = (mode == BS_REGION) ? (uint32_t)(bs_boff(d) / kBlk) : 0u;
   return mode | (l << 2) | (U << 7) | (bblk << 16);
+}
+// meta of slot (u -> x) with c common neighbours (u's row is [ub, ue))
+__device__ __forceinline__ uint32_t bs_meta_slot(const gw_dev_graph& G, uint32_t c, uint32_t d, int32_t u, int64_t ub,
+                                                 int64_t ue) {
+  if (c == 0u && d < GW_BS_PACK_D && gw_row_find(G.nbrs, ub, ue, u) < 0) return kMetaStashOk;  // list mode, meta 0
+  return bs_meta(c, d);
 }
 
 // first index in [b, e) with nbrs[i] >= key
@@ -404,7 +419,7 @@ __global__ void k_bs_fill_small(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn) {
     }
   }
   en.r[0] = kp | (c << 16);  // d <= 32: packed header, payload r[1..11]
-  en.meta = bs_meta(c, (uint32_t)d);
+  en.meta = bs_meta_slot(G, c, (uint32_t)d, u, ub, ue);
   if (gw_bs_is_list(c, (uint32_t)d)) {  // sorted positions, 0xFFFF padded
     uint16_t* lp = reinterpret_cast<uint16_t*>(en.r + 1);
     for (int t = 0; t < 2 * 11; ++t) lp[t] = 0xFFFFu;
@@ -429,7 +444,7 @@ __global__ void k_bs_fill_thread(gw_dev_graph G, const uint64_t* __restrict__ ro
   gw_bs_nbr* en = bsn + e;
   const uint32_t c = bs_c(en, (uint32_t)d);
   uint32_t* w = bs_payload(en, (uint32_t)d);
-  en->meta = bs_meta(c, (uint32_t)d);
+  en->meta = bs_meta_slot(G, c, (uint32_t)d, S.u, S.ub, S.ue);
   if (lists_only && bs_mode(c, (uint32_t)d) == BS_REGION) {  // no payload: a draw filter, the walk probes
     common_thread(G, S, [&](int64_t k, uint32_t, int64_t) { bs_filter_only(w, k, (uint32_t)d); });
     return;
@@ -461,18 +476,19 @@ __global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff
     gw_bs_nbr* en = bsn + e;
     const uint32_t d = en->d, c = bs_c(en, d);
     uint32_t* w = bs_payload(en, d);
+    const BsSlot S = bs_slot(G, e);
     if (lists_only && bs_mode(c, d) == BS_REGION) {  // no payload: a draw filter, the walk probes
       if (lane == 0) en->meta = bs_meta(c, d);
       int64_t kl;
-      common_wave(G, bs_slot(G, e), [&](int64_t k, uint32_t, int64_t) { bs_filter_only(w, k, d); }, &kl);
+      common_wave(G, S, [&](int64_t k, uint32_t, int64_t) { bs_filter_only(w, k, d); }, &kl);
       continue;
     }
     const BsEmit E = bs_emit(en, reg, roff, e, c, d);
     if (E.mode == BS_LIST && lane >= (int)c && lane < 2 * (int)gw_bs_pw(d)) reinterpret_cast<uint16_t*>(w)[lane] = 0xFFFFu;
     if (E.mode == BS_REGION && lane == 0) w[0] = (uint32_t)(roff[e] / kBlk);
-    if (lane == 0) en->meta = bs_meta(c, d);
+    if (lane == 0) en->meta = bs_meta_slot(G, c, d, S.u, S.ub, S.ue);
     int64_t klast;
-    common_wave(G, bs_slot(G, e), E, &klast);
+    common_wave(G, S, E, &klast);
     if (E.mode == BS_REGION)
       for (int64_t g = (klast < 0 ? -1 : klast / kDirBits) + 1 + lane; g < E.ndir; g += 64) E.set_dir(g, g, c);
   }
@@ -524,8 +540,14 @@ __device__ __forceinline__ uint32_t bits32(const uint32_t (&pl)[kPW], uint32_t p
 // lw = the 32 bits at U + e0 * l (already read by the caller).
 __device__ __forceinline__ bool ef_bucket_has(const uint32_t (&pl)[kPW], uint32_t U, uint32_t l, uint32_t s,
                                               uint32_t e0, uint32_t k, uint32_t lw) {
-  const uint32_t hw = bits32(pl, s);  // the run of ones ends at a zero below U
-  const uint32_t run = hw == 0xFFFFFFFFu ? 32u : (uint32_t)__builtin_ctz(~hw);
+  // the run of ones ends at a zero below U; a bucket spans 2^l positions, so
+  // it can hold more than 32 elements (l >= 6): keep reading windows
+  uint32_t hw = bits32(pl, s), run = 0;
+  while (hw == 0xFFFFFFFFu && run < 320u) {
+    run += 32u;
+    hw = bits32(pl, s + run);
+  }
+  run += (uint32_t)__builtin_ctz(~hw);
   if (l == 0) return run > 0;
   const uint32_t mask = (1u << l) - 1u, lowk = k & mask;
   uint32_t o = 0;
@@ -786,7 +808,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
         isblk = true;
       }
       if (acc) {
-        if ((meta >> 31) && k == (int64_t)kp) {
+        if (meta == kMetaStash && k == (int64_t)kp) {
           // return over an edge with no common neighbours: the entry of the
           // reverse slot (cur -> prev) is {prev, its degree and row, kp = the
           // index drawn at prev, c = 0, empty list}, all kept in pl[0..3]
@@ -838,14 +860,15 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
       b = E[2];
       meta = E[3];
       unpack_entry(E, &kp, &c, pl);
-      if (c == 0u && d < GW_BS_PACK_D && od < GW_BS_PACK_D) {
-        // empty list: its payload words keep the row we came from (a later
-        // return needs no fetch); bit 31 of meta marks the stash (list mode)
+      if (meta == kMetaStashOk && od < GW_BS_PACK_D) {
+        // empty list (and c(cur -> ou) = 0 too): its payload words keep the
+        // row we came from (a later return needs no fetch); kMetaStash marks
+        // the stash (list mode)
         pl[0] = ou;
         pl[1] = od;
         pl[2] = ob;
         pl[3] = ok;
-        meta = 0x80000000u;
+        meta = kMetaStash;
       }
     }
     if (virt) {  // swap the current row and the stash: the walker is back at prev

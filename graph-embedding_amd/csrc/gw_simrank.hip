@@ -382,7 +382,7 @@ int gw_dev_simrank_naive(gw_graph* g, double C, int iters, double* sim_dev, void
 
 extern "C" int gw_simrank_naive_host(gw_graph* g, double C, int iters, double* sim) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);  // restores the caller's current device on return
+  GW_GUARD_DEVICE(g, g->device);  // restores the caller's current device on return
   if (g->device < 0) return gw_fail(g, GW_ERR_STATE, "graph is not on a device");
   if (g->directed) return gw_fail(g, GW_ERR_UNSUPPORTED, "naive SimRank needs an undirected graph");
   if (g->n > 0 && !sim) return gw_fail(g, GW_ERR_INVALID, "bad arguments");

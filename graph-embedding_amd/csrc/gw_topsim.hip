@@ -57,6 +57,7 @@ struct TsArgs {
   int32_t* out_ids;
   double* out_scores;
   double* out_rows;
+  gw_ts_sparse sp;  // sparse rows (sp.cursor != nullptr): nonzero (id, score) entries per source
   long long* stats;
   int64_t level_cap, spawn_cap, touch_cap;
   int32_t* lvl_vertex;
@@ -197,7 +198,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   __shared__ long long s_red[TS_WAVES];
   __shared__ int s_size[L + 2];
   __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount, s_bin, s_cum, s_exact, s_total;
-  __shared__ unsigned long long s_prefix, s_mask;
+  __shared__ unsigned long long s_prefix, s_mask, s_spbase;
   // the output phase's selection arrays share LDS with the levels' child
   // offsets / the walkers' spawner offsets (binary-searched per child / walker)
   __shared__ union {
@@ -634,6 +635,40 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         }
       }
     }
+    if (A.sp.cursor) {
+      // sparse row: every nonzero entry (accumulator order), packed at a
+      // claimed offset; a row that does not fit is skipped (len -1) but still
+      // counted, so the cursor ends at the room all rows need
+      int mine = 0;
+      for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+        int32_t id;
+        double v;
+        mine += cand(idx, &id, &v) ? 1 : 0;
+      }
+      int tot;
+      const int ex = block_excl_scan(mine, s_wave, &tot);
+      if (tid == 0) s_spbase = atomicAdd(A.sp.cursor, (unsigned long long)tot);
+      __syncthreads();
+      const int64_t base = (int64_t)s_spbase;
+      const bool fits = base + tot <= A.sp.cap;
+      if (fits) {
+        int64_t o = base + ex;
+        for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+          int32_t id;
+          double v;
+          if (cand(idx, &id, &v)) {
+            A.sp.ids[o] = id;
+            A.sp.scores[o] = v;
+            ++o;
+          }
+        }
+      }
+      if (tid == 0) {
+        A.sp.begin[r] = fits ? base : -1;
+        A.sp.len[r] = fits ? tot : -1;
+        if (!fits) atomicOr(A.error_flag, 4);
+      }
+    }
     if (A.out_ids) {
       const int K = A.topk;
       // the K-th key's bin may be taken whole once everything at or above it
@@ -1014,7 +1049,8 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
 
 int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint64_t seed,
                   const int32_t* sources_dev, int64_t nsrc, int topk, int32_t* out_ids_dev,
-                  double* out_scores_dev, double* out_rows_dev, int64_t* stats_dev, void* stream) {
+                  double* out_scores_dev, double* out_rows_dev, int64_t* stats_dev, void* stream,
+                  const gw_ts_sparse* sparse) {
   gw_topsim_ws& t = g->ts;
   if (t.blocks == 0 || t.variant != variant || t.sample != sample || t.step != step ||
       (out_ids_dev && topk > t.topk)) {
@@ -1043,6 +1079,7 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   A.out_ids = out_ids_dev;
   A.out_scores = out_scores_dev;
   A.out_rows = out_rows_dev;
+  A.sp = sparse ? *sparse : gw_ts_sparse{};
   A.stats = (long long*)stats_dev;
   A.level_cap = t.level_cap;
   A.spawn_cap = t.spawn_cap;
@@ -1090,8 +1127,12 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
                  blocks, ph[0] + 0ull, ph[2], ph[3] + ph[5] + ph[6] + ph[7] + ph[8] + ph[9], ph[5], ph[6], ph[7],
                  ph[8], ph[9], ph[4], ph[1]);
   }
-  if (flag) {
+  if (flag & 3) {
     g->err = "TopSim frontier exceeded the workspace (level/spawn/touch capacity)";
+    return GW_ERR_CAPACITY;
+  }
+  if (flag & 4) {
+    g->err = "sparse rows exceed the output capacity (rows with len -1 did not fit; *used = room needed)";
     return GW_ERR_CAPACITY;
   }
   return GW_OK;
@@ -1104,7 +1145,7 @@ extern "C" int gw_topsim_host(gw_graph* g, int variant, int sample, int step, do
                               const int32_t* sources, int64_t nsrc, int topk, int32_t* out_ids,
                               double* out_scores, double* out_rows, int64_t* stats) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);  // restores the caller's current device on return
+  GW_GUARD_DEVICE(g, g->device);  // restores the caller's current device on return
   if (g->device < 0) return gw_fail(g, GW_ERR_STATE, "graph is not on a device");
   if (nsrc < 0 || (nsrc > 0 && !sources) || (!out_rows && (!out_ids || !out_scores)) || topk < 0)
     return gw_fail(g, GW_ERR_INVALID, "bad arguments");
@@ -1146,5 +1187,99 @@ extern "C" int gw_topsim_host(gw_graph* g, int variant, int sample, int step, do
   ws_free(d_src); ws_free(d_st); ws_free(d_rows); ws_free(d_ids); ws_free(d_sc);
   if (rc != GW_OK) return rc;
   if (e != hipSuccess) return gw_fail(g, GW_ERR_DEVICE, "%s", hipGetErrorString(e));
+  return GW_OK;
+}
+
+// TopSim compute() + Print.printByOrder in one call, Java-exact at any V
+// (TopSim_singleSample.java:47-54, Print.java:25-53): sources in batches
+// through HBM as sparse rows (gw_topsim_sparse), each batch replayed through
+// FixedMaxPQ on the host and appended to path / path.sim.txt in source order.
+extern "C" int gw_topsim_write_text(gw_graph* g, int variant, int sample, int step, double C, uint64_t seed,
+                                    const int32_t* sources, int64_t nsrc, int topk, const char* path, const char* sep,
+                                    int decimals, int64_t* stats) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  GW_GUARD_DEVICE(g, g->device);
+  if (g->device < 0) return gw_fail(g, GW_ERR_STATE, "graph is not on a device");
+  if (nsrc < 0 || (nsrc > 0 && !sources) || topk < 0 || !path || decimals < 0 || decimals > 30)
+    return gw_fail(g, GW_ERR_INVALID, "bad arguments");
+  for (int64_t i = 0; i < nsrc; ++i)
+    if (sources[i] < 0 || sources[i] >= g->n) return gw_fail(g, GW_ERR_RANGE, "source %d out of [0,V)", sources[i]);
+  const std::string sp_sep = sep ? sep : ",";
+  std::string err;
+  int rc = gw_write_sim_sparse_impl(path, nullptr, nullptr, nullptr, nullptr, nullptr, 0, g->n, topk, sp_sep,
+                                    decimals, false, &err);  // create / truncate both files
+  if (rc != GW_OK) return gw_fail(g, rc, "%s", err.c_str());
+  GW_HIP_TRY(hipSetDevice(g->device));
+  const int64_t n = g->n;
+  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(nsrc, 65536));
+  int64_t cap = std::max<int64_t>(1, std::min<int64_t>(chunk * n, (int64_t)1 << 26));
+  int32_t *d_src = nullptr, *d_len = nullptr, *d_ids = nullptr;
+  int64_t *d_begin = nullptr, *d_used = nullptr, *d_st = nullptr;
+  double* d_sc = nullptr;
+  auto release = [&]() {
+    ws_free(d_src); ws_free(d_len); ws_free(d_ids); ws_free(d_begin); ws_free(d_used); ws_free(d_st); ws_free(d_sc);
+  };
+  if ((rc = ws_alloc(g, &d_src, chunk)) || (rc = ws_alloc(g, &d_len, chunk)) || (rc = ws_alloc(g, &d_begin, chunk)) ||
+      (rc = ws_alloc(g, &d_used, 1)) || (rc = ws_alloc(g, &d_st, 4)) || (rc = ws_alloc(g, &d_ids, cap)) ||
+      (rc = ws_alloc(g, &d_sc, cap))) {
+    release();
+    return rc;
+  }
+  int64_t tot_st[4] = {0, 0, 0, 0};
+  std::vector<int64_t> h_begin;
+  std::vector<int32_t> h_len, h_ids;
+  std::vector<double> h_sc;
+  hipError_t e = hipSuccess;
+  for (int64_t c0 = 0; c0 < nsrc && rc == GW_OK;) {
+    const int64_t cn = std::min(chunk, nsrc - c0);
+    if ((e = hipMemcpy(d_src, sources + c0, cn * sizeof(int32_t), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemset(d_st, 0, 4 * sizeof(int64_t))) != hipSuccess || (e = hipMemset(d_used, 0, sizeof(int64_t))) != hipSuccess)
+      break;
+    gw_ts_sparse sp;
+    sp.cap = cap;
+    sp.begin = d_begin;
+    sp.len = d_len;
+    sp.ids = d_ids;
+    sp.scores = d_sc;
+    sp.cursor = reinterpret_cast<unsigned long long*>(d_used);
+    rc = gw_dev_topsim(g, variant, sample, step, C, seed, d_src, cn, 0, nullptr, nullptr, nullptr, d_st, nullptr, &sp);
+    int64_t used = 0;
+    if ((e = hipMemcpy(&used, d_used, sizeof(int64_t), hipMemcpyDeviceToHost)) != hipSuccess) break;
+    if (rc == GW_ERR_CAPACITY && used > cap) {  // the rows need more room: grow and redo this batch
+      cap = used + used / 8;
+      ws_free(d_ids);
+      ws_free(d_sc);
+      if ((rc = ws_alloc(g, &d_ids, cap)) || (rc = ws_alloc(g, &d_sc, cap))) break;
+      continue;
+    }
+    if (rc != GW_OK) break;
+    int64_t st[4];
+    h_begin.resize(cn);
+    h_len.resize(cn);
+    h_ids.resize(std::max<int64_t>(used, 1));
+    h_sc.resize(std::max<int64_t>(used, 1));
+    if ((e = hipMemcpy(st, d_st, sizeof st, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(h_begin.data(), d_begin, cn * sizeof(int64_t), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(h_len.data(), d_len, cn * sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (used > 0 && (e = hipMemcpy(h_ids.data(), d_ids, used * sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess) ||
+        (used > 0 && (e = hipMemcpy(h_sc.data(), d_sc, used * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess))
+      break;
+    tot_st[0] += st[0];
+    tot_st[1] += st[1];
+    tot_st[2] = std::max(tot_st[2], st[2]);
+    tot_st[3] += st[3];
+    rc = gw_write_sim_sparse_impl(path, h_begin.data(), h_len.data(), h_ids.data(), h_sc.data(), sources + c0, cn, n,
+                                  topk, sp_sep, decimals, true, &err);
+    if (rc != GW_OK) {
+      gw_fail(g, rc, "%s", err.c_str());
+      break;
+    }
+    c0 += cn;
+  }
+  release();
+  if (rc != GW_OK) return rc;
+  if (e != hipSuccess) return gw_fail(g, GW_ERR_DEVICE, "%s", hipGetErrorString(e));
+  if (stats)
+    for (int k = 0; k < 4; ++k) stats[k] = tot_st[k];
   return GW_OK;
 }

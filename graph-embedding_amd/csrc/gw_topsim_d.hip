@@ -684,7 +684,7 @@ int gw_dev_double_random_walk(gw_graph* g, int sample, int step, double C, uint6
 extern "C" int gw_double_sim_host(gw_graph* g, int kind, int sample, int step, int topK, int singleStep, double C,
                        uint64_t seed, const int32_t* cand, double* sim) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);  // restores the caller's current device on return
+  GW_GUARD_DEVICE(g, g->device);  // restores the caller's current device on return
   if (g->device < 0) return gw_fail(g, GW_ERR_STATE, "graph is not on a device");
   if (g->n > 0 && !sim) return gw_fail(g, GW_ERR_INVALID, "bad arguments");
   if (kind == GW_DOUBLE_DEV && topK > 0 && !cand) return gw_fail(g, GW_ERR_INVALID, "candidates required");

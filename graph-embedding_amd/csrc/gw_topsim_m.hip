@@ -583,7 +583,7 @@ extern "C" int gw_topsim_m_host(gw_graph* g, int variant, int capacity, int samp
                                 uint64_t seed, const int32_t* sources, int64_t nsrc, int32_t* out_keys,
                                 float* out_vals, int32_t* out_size, int64_t* stats) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
-  gw_device_guard dg(g->device);  // restores the caller's current device on return
+  GW_GUARD_DEVICE(g, g->device);  // restores the caller's current device on return
   if (g->device < 0) return gw_fail(g, GW_ERR_STATE, "graph is not on a device");
   if (nsrc < 0 || (nsrc > 0 && (!sources || !out_keys || !out_vals || !out_size)) || capacity < 1)
     return gw_fail(g, GW_ERR_INVALID, "bad arguments");

@@ -114,6 +114,10 @@ SIGNATURES = {
                                  ctypes.c_int, P, P, P, P]),
     "gw_topsim_dense": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, U64, P, I64,
                                        P, P, P]),
+    "gw_topsim_sparse": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, U64, P, I64, I64,
+                                        P, P, P, P, P, P, P]),
+    "gw_topsim_write_text": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, U64, P, I64,
+                                            ctypes.c_int, CP, CP, ctypes.c_int, P]),
     "gw_topsim_m": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, U64, P, I64,
                                    P, P, P, P, P]),
     "gw_topsim_m_host": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, U64, P,
@@ -130,6 +134,7 @@ SIGNATURES = {
     "gw_write_walks_text": (ctypes.c_int, [P, CP, P, P, I64, ctypes.c_int]),
     "gw_write_sim_text_dense": (ctypes.c_int, [CP, P, P, I64, I64, ctypes.c_int, CP, ctypes.c_int]),
     "gw_write_sim_text_topk": (ctypes.c_int, [CP, P, P, P, I64, ctypes.c_int, CP, ctypes.c_int]),
+    "gw_write_sim_text_sparse": (ctypes.c_int, [CP, P, P, P, P, P, I64, I64, ctypes.c_int, CP, ctypes.c_int]),
     "gw_write_sim_text_cachemap": (ctypes.c_int, [CP, P, P, P, P, I64, ctypes.c_int, ctypes.c_int, CP]),
     "gw_comm_unique_id": (ctypes.c_int, [P]),
     "gw_comm_init": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, PP]),

@@ -127,6 +127,56 @@ class _TopSimBase:
         full[self._sources] = self._rows
         return full
 
+    def sparse(self, sources=None, capacity=None):
+        """Nonzero (id, score) entries of each source's row (gw_topsim_sparse):
+        returns (row_begin, row_len, ids, scores) host arrays, entries of a row
+        in no particular order."""
+        import torch
+        src = self._default_sources() if sources is None else np.asarray(sources, np.int32)
+        g = self.g
+        g._ensure_device()
+        dev = torch.device("cuda", g.device)
+        h = g._g.handle
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        s_dev = torch.as_tensor(np.ascontiguousarray(src, np.int32), device=dev)
+        cap = int(capacity) if capacity is not None else max(1, min(len(src) * self.COUNT, 1 << 24))
+        while True:
+            begin = torch.empty(len(src), dtype=torch.int64, device=dev)
+            ln = torch.empty(len(src), dtype=torch.int32, device=dev)
+            ids = torch.empty(cap, dtype=torch.int32, device=dev)
+            sc = torch.empty(cap, dtype=torch.float64, device=dev)
+            used = torch.zeros(1, dtype=torch.int64, device=dev)
+            stats = torch.zeros(4, dtype=torch.int64, device=dev)
+            rc = C.lib().gw_topsim_sparse(h, self.VARIANT, self.SAMPLE, self.STEP, self.C, self.seed,
+                                          C.ptr(s_dev), len(src), cap, C.ptr(begin), C.ptr(ln), C.ptr(ids),
+                                          C.ptr(sc), C.ptr(used), C.ptr(stats), stream)
+            need = int(used.cpu()[0])
+            if rc == C.GW_ERR_CAPACITY and need > cap:
+                cap = need
+                continue
+            C.check(rc, h)
+            break
+        s = stats.cpu().numpy()
+        self.stats = dict(extensions=int(s[0]), pair_updates=int(s[1]), max_frontier=int(s[2]),
+                          walkers=int(s[3]))
+        return begin.cpu().numpy(), ln.cpu().numpy(), ids[:need].cpu().numpy(), sc[:need].cpu().numpy()
+
+    def writeText(self, outPath, topk=TOPK, sources=None, separator=SEPARATOR, decimals=6):
+        """compute() + Print.printByOrder in one native call
+        (gw_topsim_write_text): Java-exact bytes at any V."""
+        src = self._sources if sources is None else np.asarray(sources, np.int32)
+        if src is None:
+            src = self._default_sources()
+        src = np.ascontiguousarray(src, np.int32)
+        self.g._ensure_device()
+        st = np.zeros(4, np.int64)
+        h = self.g._g.handle
+        C.check(C.lib().gw_topsim_write_text(h, self.VARIANT, self.SAMPLE, self.STEP, self.C, self.seed,
+                                             C.ptr(src), len(src), int(topk), str(outPath).encode(),
+                                             separator.encode(), int(decimals), C.ptr(st)), h)
+        self.stats = dict(extensions=int(st[0]), pair_updates=int(st[1]), max_frontier=int(st[2]),
+                          walkers=int(st[3]))
+
     def topK(self, k=TOPK, sources=None):
         src = self._default_sources() if sources is None else np.asarray(sources, np.int32)
         return self._run(src, topk=k)
@@ -396,14 +446,9 @@ def printByOrder(sim, outPath, topk=TOPK, testTopK=None, separator=SEPARATOR, de
                                                     rows.shape[0], rows.shape[1], int(topk),
                                                     separator.encode(), int(decimals)))
             return
-        ids, sc = sim._topk if sim._topk is not None else sim.topK(topk)
-        ids = np.ascontiguousarray(ids, np.int32)
-        sc = np.ascontiguousarray(sc, np.float64)
-        rid = np.ascontiguousarray(sim._sources if sim._sources is not None else np.arange(ids.shape[0]),
-                                   np.int32)
-        C.check(C.lib().gw_write_sim_text_topk(str(outPath).encode(), C.ptr(ids), C.ptr(sc), C.ptr(rid),
-                                               ids.shape[0], ids.shape[1], separator.encode(),
-                                               int(decimals)))
+        # rows too large to keep dense: recompute the same Philox walks as
+        # sparse rows and replay FixedMaxPQ exactly (gw_topsim_write_text)
+        sim.writeText(outPath, topk, separator=separator, decimals=decimals)
         return
     rows = np.ascontiguousarray(sim, np.float64)
     C.check(C.lib().gw_write_sim_text_dense(str(outPath).encode(), C.ptr(rows), None, rows.shape[0],

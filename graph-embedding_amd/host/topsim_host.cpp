@@ -84,6 +84,12 @@ void TopSimBase::compute(const std::vector<int32_t>& sources) {
   stats_.walkers = st[3];
 }
 
+void TopSimBase::writeText(const std::string& outPath, int topk, const std::string& sep, int decimals) const {
+  gw::check(gw_topsim_write_text(g_.handle(), variant_, SAMPLE, STEP, conf::MyConfiguration::C, seed_, sources_.data(),
+                                 (int64_t)sources_.size(), topk, outPath.c_str(), sep.c_str(), decimals, nullptr),
+            g_.handle());
+}
+
 const std::vector<double>& TopSimBase::getResult() const {
   if (!dense_) throw gw::Error(GW_ERR_STATE, "dense result not kept (V too large); use topK()");
   return sim_;
@@ -159,9 +165,7 @@ void Print::printByOrder(const simrank::TopSimBase& sim, const std::string& outP
     gw::check(gw_write_sim_text_dense(outPath.c_str(), rows.data(), sim.sources().data(),
                                       (int64_t)sim.sources().size(), sim.getVCount(), topk, sep.c_str(), 6));
   } else {
-    gw::check(gw_write_sim_text_topk(outPath.c_str(), sim.topk_ids().data(), sim.topk_scores().data(),
-                                     sim.sources().data(), (int64_t)sim.sources().size(), sim.topk_rows_k(),
-                                     sep.c_str(), 6));
+    sim.writeText(outPath, topk, sep, 6);  // Java-exact from sparse rows
   }
 }
 

@@ -79,6 +79,10 @@ class TopSimBase {
   // sparse top-k rows: ids[src*k + j] (-1 padded), scores likewise
   void topK(int k, std::vector<int32_t>& ids, std::vector<double>& scores,
             const std::vector<int32_t>* sources = nullptr) const;
+  // compute() + Print.printByOrder(sim, outPath, topk) for rows too large to
+  // keep dense: the same Philox walks as sparse rows, FixedMaxPQ replayed
+  // exactly (gw_topsim_write_text)
+  void writeText(const std::string& outPath, int topk, const std::string& sep, int decimals) const;
   gw_topsim_stats_t stats() const { return stats_; }
   const std::vector<int32_t>& sources() const { return sources_; }
   bool dense() const { return dense_; }

@@ -30,12 +30,28 @@ static void throw_gw(JNIEnv* env, int rc, const gw_graph* g) {
 
 static gw_graph* G(jlong h) { return (gw_graph*)(intptr_t)h; }
 
+static void throw_arg(JNIEnv* env, const char* msg) {
+  jclass c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+  if (c) (*env)->ThrowNew(env, c, msg);
+}
+
+/* a Get*ArrayElements / GetStringUTFChars that returned NULL has already
+ * thrown (OutOfMemoryError): the caller releases what it pinned and returns */
+
 /* structures.Graph(path, V) with MyConfiguration.SEPARATOR (Graph.java:28-42), uploaded to `device` */
 JNIEXPORT jlong JNICALL Java_simrank_GraphWalkNative_loadGraph(JNIEnv* env, jclass cls, jstring path, jstring sep,
                                                                jint V, jint device) {
   (void)cls;
+  if (!path || !sep) {
+    throw_arg(env, "path / separator is null");
+    return 0;
+  }
   const char* p = (*env)->GetStringUTFChars(env, path, 0);
-  const char* s = (*env)->GetStringUTFChars(env, sep, 0);
+  const char* s = p ? (*env)->GetStringUTFChars(env, sep, 0) : NULL;
+  if (!p || !s) {
+    if (p) (*env)->ReleaseStringUTFChars(env, path, p);
+    return 0;
+  }
   gw_graph* g = NULL;
   int rc = gw_graph_load_edgelist(p, s, GW_SEM_JAVA_MULTI, 0, 0, V, &g);
   if (rc == GW_OK) rc = gw_graph_to_device(g, device);
@@ -73,22 +89,67 @@ JNIEXPORT void JNICALL Java_simrank_GraphWalkNative_topsimTopK(JNIEnv* env, jcla
                                                                jdoubleArray scoresOut, jlongArray stats) {
   (void)cls;
   gw_graph* g = G(gh);
-  jsize ns = (*env)->GetArrayLength(env, sources);
-  if ((*env)->GetArrayLength(env, idsOut) < (jsize)ns * k || (*env)->GetArrayLength(env, scoresOut) < (jsize)ns * k) {
-    jclass c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
-    if (c) (*env)->ThrowNew(env, c, "idsOut / scoresOut shorter than sources.length * k");
+  if (!sources || !idsOut || !scoresOut || k < 0) {
+    throw_arg(env, "null array or k < 0");
+    return;
+  }
+  const jsize ns = (*env)->GetArrayLength(env, sources);
+  const int64_t need = (int64_t)ns * (int64_t)k; /* 64-bit: ns * k can pass 2^31 */
+  if ((int64_t)(*env)->GetArrayLength(env, idsOut) < need || (int64_t)(*env)->GetArrayLength(env, scoresOut) < need) {
+    throw_arg(env, "idsOut / scoresOut shorter than sources.length * k");
+    return;
+  }
+  if (stats && (*env)->GetArrayLength(env, stats) < 4) {
+    throw_arg(env, "stats needs 4 entries");
     return;
   }
   jint* src = (*env)->GetIntArrayElements(env, sources, 0);
-  jint* ids = (*env)->GetIntArrayElements(env, idsOut, 0);
-  jdouble* sc = (*env)->GetDoubleArrayElements(env, scoresOut, 0);
-  jlong* st = stats ? (*env)->GetLongArrayElements(env, stats, 0) : NULL;
-  int rc = gw_topsim_host(g, variant, sample, step, C, (uint64_t)seed, (const int32_t*)src, ns, k, (int32_t*)ids, sc,
-                          NULL, (int64_t*)st);
-  (*env)->ReleaseIntArrayElements(env, sources, src, JNI_ABORT);
-  (*env)->ReleaseIntArrayElements(env, idsOut, ids, 0);
-  (*env)->ReleaseDoubleArrayElements(env, scoresOut, sc, 0);
+  jint* ids = src ? (*env)->GetIntArrayElements(env, idsOut, 0) : NULL;
+  jdouble* sc = ids ? (*env)->GetDoubleArrayElements(env, scoresOut, 0) : NULL;
+  jlong* st = (sc && stats) ? (*env)->GetLongArrayElements(env, stats, 0) : NULL;
+  int rc = GW_ERR_NOMEM;
+  if (src && ids && sc && (!stats || st))
+    rc = gw_topsim_host(g, variant, sample, step, C, (uint64_t)seed, (const int32_t*)src, ns, k, (int32_t*)ids, sc,
+                        NULL, (int64_t*)st);
+  if (src) (*env)->ReleaseIntArrayElements(env, sources, src, JNI_ABORT);
+  if (ids) (*env)->ReleaseIntArrayElements(env, idsOut, ids, 0);
+  if (sc) (*env)->ReleaseDoubleArrayElements(env, scoresOut, sc, 0);
   if (st) (*env)->ReleaseLongArrayElements(env, stats, st, 0);
+  if ((*env)->ExceptionCheck(env)) return; /* a pin failed: OutOfMemoryError pending */
+  if (rc != GW_OK) throw_gw(env, rc, g);
+}
+
+/* TopSim compute() + utils.Print.printByOrder (TopSim_singleSample.java:47-54,
+ * Print.java:25-53) for `sources`, Java-exact at any V (gw_topsim_write_text:
+ * sparse rows, FixedMaxPQ replayed): path and path + ".sim.txt" */
+JNIEXPORT void JNICALL Java_simrank_GraphWalkNative_topsimWriteText(JNIEnv* env, jclass cls, jlong gh, jint variant,
+                                                                    jint sample, jint step, jdouble C, jlong seed,
+                                                                    jintArray sources, jint topk, jstring path,
+                                                                    jstring sep, jlongArray stats) {
+  (void)cls;
+  gw_graph* g = G(gh);
+  if (!sources || !path || !sep || topk < 0) {
+    throw_arg(env, "null argument or topk < 0");
+    return;
+  }
+  if (stats && (*env)->GetArrayLength(env, stats) < 4) {
+    throw_arg(env, "stats needs 4 entries");
+    return;
+  }
+  const jsize ns = (*env)->GetArrayLength(env, sources);
+  const char* p = (*env)->GetStringUTFChars(env, path, 0);
+  const char* s = p ? (*env)->GetStringUTFChars(env, sep, 0) : NULL;
+  jint* src = s ? (*env)->GetIntArrayElements(env, sources, 0) : NULL;
+  jlong* st = (src && stats) ? (*env)->GetLongArrayElements(env, stats, 0) : NULL;
+  int rc = GW_ERR_NOMEM;
+  if (p && s && src && (!stats || st))
+    rc = gw_topsim_write_text(g, variant, sample, step, C, (uint64_t)seed, (const int32_t*)src, ns, topk, p, s, 6,
+                              (int64_t*)st);
+  if (st) (*env)->ReleaseLongArrayElements(env, stats, st, 0);
+  if (src) (*env)->ReleaseIntArrayElements(env, sources, src, JNI_ABORT);
+  if (s) (*env)->ReleaseStringUTFChars(env, sep, s);
+  if (p) (*env)->ReleaseStringUTFChars(env, path, p);
+  if ((*env)->ExceptionCheck(env)) return;
   if (rc != GW_OK) throw_gw(env, rc, g);
 }
 
@@ -104,26 +165,42 @@ JNIEXPORT void JNICALL Java_simrank_GraphWalkNative_topsimDense(JNIEnv* env, jcl
     throw_gw(env, GW_ERR_INVALID, g);
     return;
   }
-  jsize ns = (*env)->GetArrayLength(env, sources);
+  if (!sources || !simOut) {
+    throw_arg(env, "null array");
+    return;
+  }
+  const jsize ns = (*env)->GetArrayLength(env, sources);
+  if ((*env)->GetArrayLength(env, simOut) < ns || (stats && (*env)->GetArrayLength(env, stats) < 4)) {
+    throw_arg(env, "simOut shorter than sources.length or stats shorter than 4");
+    return;
+  }
   double* rows = (double*)malloc(sizeof(double) * (size_t)ns * (size_t)(inf.n > 0 ? inf.n : 1));
   if (!rows) {
     throw_gw(env, GW_ERR_NOMEM, g);
     return;
   }
   jint* src = (*env)->GetIntArrayElements(env, sources, 0);
-  jlong* st = stats ? (*env)->GetLongArrayElements(env, stats, 0) : NULL;
-  int rc = gw_topsim_host(g, variant, sample, step, C, (uint64_t)seed, (const int32_t*)src, ns, 0, NULL, NULL, rows,
-                          (int64_t*)st);
-  (*env)->ReleaseIntArrayElements(env, sources, src, JNI_ABORT);
+  jlong* st = (src && stats) ? (*env)->GetLongArrayElements(env, stats, 0) : NULL;
+  int rc = GW_ERR_NOMEM;
+  if (src && (!stats || st))
+    rc = gw_topsim_host(g, variant, sample, step, C, (uint64_t)seed, (const int32_t*)src, ns, 0, NULL, NULL, rows,
+                        (int64_t*)st);
+  if (src) (*env)->ReleaseIntArrayElements(env, sources, src, JNI_ABORT);
   if (st) (*env)->ReleaseLongArrayElements(env, stats, st, 0);
   if (rc == GW_OK) {
-    for (jsize r = 0; r < ns; ++r) {
+    for (jsize r = 0; r < ns && !(*env)->ExceptionCheck(env); ++r) {
       jdoubleArray row = (jdoubleArray)(*env)->GetObjectArrayElement(env, simOut, r);
+      if (!row || (*env)->GetArrayLength(env, row) < (jsize)inf.n) {
+        if (row) (*env)->DeleteLocalRef(env, row);
+        throw_arg(env, "simOut row null or shorter than V");
+        break;
+      }
       (*env)->SetDoubleArrayRegion(env, row, 0, (jsize)inf.n, rows + (size_t)r * (size_t)inf.n);
       (*env)->DeleteLocalRef(env, row);
     }
   }
   free(rows);
+  if ((*env)->ExceptionCheck(env)) return;
   if (rc != GW_OK) throw_gw(env, rc, g);
 }
 
@@ -132,28 +209,50 @@ JNIEXPORT void JNICALL Java_simrank_GraphWalkNative_simrankNaive(JNIEnv* env, jc
                                                                  jint step, jdoubleArray out) {
   (void)cls;
   gw_graph* g = G(gh);
+  gw_graph_info_t inf;
+  if (gw_graph_info(g, &inf) != GW_OK) {
+    throw_gw(env, GW_ERR_INVALID, g);
+    return;
+  }
+  if (!out || (int64_t)(*env)->GetArrayLength(env, out) < (int64_t)inf.n * inf.n) {
+    throw_arg(env, "out shorter than V * V");
+    return;
+  }
   jdouble* sim = (*env)->GetDoubleArrayElements(env, out, 0);
+  if (!sim) return;
   int rc = gw_simrank_naive_host(g, C, step, sim);
   (*env)->ReleaseDoubleArrayElements(env, out, sim, 0);
   if (rc != GW_OK) throw_gw(env, rc, g);
 }
 
-/* utils.Print.printByOrder (Print.java:25-53) from top-k rows: path and path + ".sim.txt" */
+/* utils.Print.printByOrder (Print.java:25-53) layout from top-k rows as topsimTopK returns them (score desc,
+ * id asc): NOT the reference's bytes when rows have ties or fewer than k nonzeros — topsimWriteText is */
 JNIEXPORT void JNICALL Java_simrank_GraphWalkNative_writeTopK(JNIEnv* env, jclass cls, jstring path, jintArray ids,
                                                               jdoubleArray scores, jintArray rowIds, jint k,
                                                               jstring sep) {
   (void)cls;
+  if (!path || !ids || !scores || !rowIds || !sep || k < 0) {
+    throw_arg(env, "null argument or k < 0");
+    return;
+  }
+  const jsize nr = (*env)->GetArrayLength(env, rowIds);
+  const int64_t need = (int64_t)nr * (int64_t)k;
+  if ((int64_t)(*env)->GetArrayLength(env, ids) < need || (int64_t)(*env)->GetArrayLength(env, scores) < need) {
+    throw_arg(env, "ids / scores shorter than rowIds.length * k");
+    return;
+  }
   const char* p = (*env)->GetStringUTFChars(env, path, 0);
-  const char* s = (*env)->GetStringUTFChars(env, sep, 0);
-  jsize nr = (*env)->GetArrayLength(env, rowIds);
-  jint* id = (*env)->GetIntArrayElements(env, ids, 0);
-  jdouble* sc = (*env)->GetDoubleArrayElements(env, scores, 0);
-  jint* rid = (*env)->GetIntArrayElements(env, rowIds, 0);
-  int rc = gw_write_sim_text_topk(p, (const int32_t*)id, sc, (const int32_t*)rid, nr, k, s, 6);
-  (*env)->ReleaseIntArrayElements(env, ids, id, JNI_ABORT);
-  (*env)->ReleaseDoubleArrayElements(env, scores, sc, JNI_ABORT);
-  (*env)->ReleaseIntArrayElements(env, rowIds, rid, JNI_ABORT);
-  (*env)->ReleaseStringUTFChars(env, path, p);
-  (*env)->ReleaseStringUTFChars(env, sep, s);
+  const char* s = p ? (*env)->GetStringUTFChars(env, sep, 0) : NULL;
+  jint* id = s ? (*env)->GetIntArrayElements(env, ids, 0) : NULL;
+  jdouble* sc = id ? (*env)->GetDoubleArrayElements(env, scores, 0) : NULL;
+  jint* rid = sc ? (*env)->GetIntArrayElements(env, rowIds, 0) : NULL;
+  int rc = GW_ERR_NOMEM;
+  if (rid) rc = gw_write_sim_text_topk(p, (const int32_t*)id, sc, (const int32_t*)rid, nr, k, s, 6);
+  if (id) (*env)->ReleaseIntArrayElements(env, ids, id, JNI_ABORT);
+  if (sc) (*env)->ReleaseDoubleArrayElements(env, scores, sc, JNI_ABORT);
+  if (rid) (*env)->ReleaseIntArrayElements(env, rowIds, rid, JNI_ABORT);
+  if (s) (*env)->ReleaseStringUTFChars(env, sep, s);
+  if (p) (*env)->ReleaseStringUTFChars(env, path, p);
+  if ((*env)->ExceptionCheck(env)) return;
   if (rc != GW_OK) throw_gw(env, rc, NULL);
 }

@@ -37,7 +37,16 @@ public final class GraphWalkNative {
     /** simrank.SimRank(g).compute() + getResult(): V*V row-major, diagonal 0 (SimRank.java:36-81). */
     public static native void simrankNaive(long g, double C, int step, double[] simOut);
 
-    /** utils.Print.printByOrder files (Print.java:25-53) from top-k rows. */
+    /**
+     * TopSim compute() + utils.Print.printByOrder(sim, path, topk, ...) for `sources`
+     * (TopSim_singleSample.java:47-54, Print.java:25-53): the reference's bytes at any V
+     * (sparse rows, FixedMaxPQ replayed exactly); stats may be null or long[4].
+     */
+    public static native void topsimWriteText(long g, int variant, int sample, int step, double C, long seed,
+                                              int[] sources, int topk, String path, String separator, long[] stats)
+            throws java.io.IOException;
+
+    /** Print.printByOrder layout from topsimTopK rows (score desc, id asc; not Java's tie order). */
     public static native void writeTopK(String path, int[] ids, double[] scores, int[] rowIds, int k,
                                         String separator);
 }

@@ -49,6 +49,12 @@ public class TopSim_singleSampleNative {
         return ids;
     }
 
+    /** compute() + Print.printByOrder(getResult(), outPath, topk, ...) for `sources`, byte-exact at any V. */
+    public void printByOrder(int[] sources, String outPath, int topk) throws java.io.IOException {
+        GraphWalkNative.topsimWriteText(g, GraphWalkNative.TOPSIM_SINGLE_SAMPLE, sample, step, MyConfiguration.C,
+                                        seed, sources, topk, outPath, MyConfiguration.SEPARATOR, null);
+    }
+
     public void close() {
         GraphWalkNative.freeGraph(g);
     }

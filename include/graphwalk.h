@@ -232,6 +232,32 @@ int gw_topsim_dense(gw_graph* g, int variant, int sample, int step, double C,
                     uint64_t seed, const int32_t* sources_dev, int64_t nsrc,
                     double* out_rows_dev, int64_t* stats_dev, void* stream);
 
+/* Sparse rows, the input of the Java-exact writer at any V (Print.java:25-53
+ * needs every nonzero score of a row, not only its top k): per source r its
+ * nonzero entries sim[sources[r]][id] > 0, in no particular order, at
+ * out_ids_dev / out_scores_dev[row_begin_dev[r] .. + row_len_dev[r]).  Rows
+ * are packed at offsets claimed in completion order, up to `capacity`
+ * entries; *used_dev (one int64, zeroed by the call) ends as the room ALL rows
+ * needed.  A row that did not fit gets row_begin = row_len = -1 and the call
+ * returns GW_ERR_CAPACITY (re-run with capacity >= *used).  Same walks, sums
+ * and stats as gw_topsim; synchronises the stream.                          */
+int gw_topsim_sparse(gw_graph* g, int variant, int sample, int step, double C,
+                     uint64_t seed, const int32_t* sources_dev, int64_t nsrc,
+                     int64_t capacity, int64_t* row_begin_dev,
+                     int32_t* row_len_dev, int32_t* out_ids_dev,
+                     double* out_scores_dev, int64_t* used_dev,
+                     int64_t* stats_dev, void* stream);
+/* new TopSim_singleSample(g, sample, step).compute() followed by
+ * Print.printByOrder(sim, path, topk, ...) (TopSim_singleSample.java:47-54,
+ * Print.java:25-53) for the given sources (host array), Java-exact at any V:
+ * batches of sparse rows replayed through FixedMaxPQ on the host, rows
+ * written in source order.  Writes path and path+".sim.txt" (sep, %.<decimals>f);
+ * stats[4] optional.                                                        */
+int gw_topsim_write_text(gw_graph* g, int variant, int sample, int step,
+                         double C, uint64_t seed, const int32_t* sources,
+                         int64_t nsrc, int topk, const char* path,
+                         const char* sep, int decimals, int64_t* stats);
+
 /* Host-buffer form of gw_topsim / gw_topsim_dense for JNI and C++ callers:
  * sources[nsrc] on the host; either out_rows[nsrc*n] (dense, getResult())
  * or out_ids/out_scores[nsrc*topk] (top-k); stats[4] optional.            */
@@ -330,7 +356,23 @@ int gw_write_walks_text(const gw_graph* g, const char* path,
 int gw_write_sim_text_dense(const char* path, const double* rows,
                             const int32_t* row_ids, int64_t nrows, int64_t n,
                             int topk, const char* sep, int decimals);
-/* Same format from top-k rows (ids/scores as produced by gw_topsim).       */
+/* Same format from sparse rows (gw_topsim_sparse, copied to the host): row r
+ * = sim[row_ids[r]][*] with the listed nonzero entries and 0.0 elsewhere
+ * (n columns).  FixedMaxPQ(topk) is replayed exactly — the first min(topk, n)
+ * ids fill the heap (zero scores included), later offers enter only when
+ * strictly larger than the heap minimum — and written in sortedElement()
+ * order: min(topk, n) entries per row, byte-identical to
+ * gw_write_sim_text_dense on the same rows.                                */
+int gw_write_sim_text_sparse(const char* path, const int64_t* row_begin,
+                             const int32_t* row_len, const int32_t* ids,
+                             const double* scores, const int32_t* row_ids,
+                             int64_t nrows, int64_t n, int topk,
+                             const char* sep, int decimals);
+/* Same format from top-k rows as produced by gw_topsim (score desc, id asc,
+ * -1 padding dropped).  NOT Java-exact: a top-k row carries neither the
+ * zero-score ids FixedMaxPQ keeps when a row has fewer than topk nonzeros
+ * nor the heap history that orders ties; use gw_write_sim_text_sparse /
+ * gw_topsim_write_text for the reference's bytes.                          */
 int gw_write_sim_text_topk(const char* path, const int32_t* ids,
                            const double* scores, const int32_t* row_ids,
                            int64_t nrows, int topk, const char* sep,

@@ -155,6 +155,72 @@ def test_sim_writer_java_exact(gw, oracle, tmp_path):
         assert ids_lines[v].decode() == f"{v}" + "".join(f",{i}" for i, _ in exp)
 
 
+def _sparse_of(rows, rng):
+    """Nonzero entries of each row, shuffled within the row (the device emits
+    them in accumulator order), packed with gaps like claimed offsets."""
+    begin, ln, ids, sc = [], [], [], []
+    pos = 0
+    for r in range(rows.shape[0]):
+        nz = np.nonzero(rows[r])[0]
+        nz = nz[rng.permutation(len(nz))]
+        pos += int(rng.integers(0, 3))  # unused room between rows
+        while len(ids) < pos:
+            ids.append(-7)
+            sc.append(-1.0)
+        begin.append(pos)
+        ln.append(len(nz))
+        ids.extend(nz.tolist())
+        sc.extend(rows[r, nz].tolist())
+        pos += len(nz)
+    return (np.array(begin, np.int64), np.array(ln, np.int32), np.array(ids, np.int32),
+            np.array(sc, np.float64))
+
+
+@pytest.mark.parametrize("topk", [0, 1, 7, 20, 57, 80])
+def test_sim_writer_sparse_equals_dense(gw, oracle, tmp_path, topk):
+    """gw_write_sim_text_sparse (the exact top-k path, rows given as their
+    nonzero entries only) == gw_write_sim_text_dense on the same rows, byte
+    for byte: FixedMaxPQ's fill with zero-score ids, strict replacement and
+    sortedElement() tie order (Print.java:30-47, FixedMaxPQ.java:30-39,
+    72-76).  Rows with many ties, few nonzeros (fewer than topk: zero ids
+    included), all-zero rows, and topk above the row length."""
+    from gwamd import _lib as C
+    rng = np.random.default_rng(5)
+    n = 57
+    rows = np.round(rng.random((60, n)) * 6) / 6  # many ties, ~1/12 zeros
+    rows[rng.random((60, n)) < 0.5] = 0.0
+    rows[3] = 0.0
+    rows[4] = 0.0
+    rows[4, [50, 2, 40]] = [0.5, 0.5, 0.25]  # fewer nonzeros than topk
+    rows[6, :] = 0.0
+    rows[6, 56] = 1.0
+    rid = np.arange(100, 160, dtype=np.int32)
+    dense = tmp_path / "d.txt"
+    sparse = tmp_path / "s.txt"
+    C.check(C.lib().gw_write_sim_text_dense(str(dense).encode(), C.ptr(np.ascontiguousarray(rows)), C.ptr(rid),
+                                            rows.shape[0], n, topk, b",", 6))
+    b, ln, ids, sc = _sparse_of(rows, rng)
+    C.check(C.lib().gw_write_sim_text_sparse(str(sparse).encode(), C.ptr(b), C.ptr(ln), C.ptr(ids), C.ptr(sc),
+                                             C.ptr(rid), rows.shape[0], n, topk, b",", 6))
+    assert open(sparse, "rb").read() == open(dense, "rb").read()
+    assert open(str(sparse) + ".sim.txt", "rb").read() == open(str(dense) + ".sim.txt", "rb").read()
+    lines = open(str(sparse) + ".sim.txt", "rb").read().split(b"\r\n")
+    for v in range(rows.shape[0]):
+        exp = oracle.java_fixed_max_pq_row(rows[v], topk) if topk else []
+        assert lines[v].decode() == f"{rid[v]}" + "".join(f",{i}:{oracle.java_format_fixed(x)}" for i, x in exp)
+        assert len(exp) == min(topk, n)
+
+
+def test_sim_writer_sparse_rejects_bad_rows(gw, tmp_path):
+    from gwamd import _lib as C
+    b = np.array([0], np.int64)
+    for ln, ids, sc in [([-1], [0], [1.0]), ([2], [3, 3], [1.0, 2.0]), ([1], [9], [1.0]), ([1], [2], [0.0])]:
+        ln, ids, sc = np.array(ln, np.int32), np.array(ids, np.int32), np.array(sc)  # alive across the call
+        rc = C.lib().gw_write_sim_text_sparse(str(tmp_path / "x").encode(), C.ptr(b), C.ptr(ln), C.ptr(ids),
+                                              C.ptr(sc), None, 1, 5, 3, b",", 6)
+        assert rc in (C.GW_ERR_INVALID, C.GW_ERR_RANGE)
+
+
 def test_sim_writer_print_by_order_all(gw, oracle, tmp_path):
     """Print.printByOrderAll (Print.java:55-84): %.7f, topk 1000 > row length."""
     from gwamd import topsim

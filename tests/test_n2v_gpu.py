@@ -351,6 +351,80 @@ def test_bitset_directory_hub_equals_oracle(gw, oracle, tmp_path, p, q):
     assert (out.cpu().numpy() == 0).sum() > count // 8  # the hub (dense id 0) is visited often
 
 
+def _selfloop_sparse_edgelist(path):
+    """Sparse graph (a random tree plus a few extra edges, mean degree ~2.6)
+    with self-loops on a third of the vertices: many edges u -> x with no
+    common neighbour next to a self-looped u, where c(u -> x) = 0 but
+    c(x -> u) = 1 (u's own loop) — the case the return elision must not
+    stash.  Starts with the minimal instance (0,0), (0,1), (1,2)."""
+    rng = np.random.default_rng(303)
+    n = 3000
+    E = {(0, 0), (0, 1), (1, 2)}
+    for v in range(3, n):
+        E.add((int(rng.integers(0, v)), v))
+    for _ in range(n // 3):
+        a, b = sorted(int(x) for x in rng.integers(0, n, 2))
+        if a != b:
+            E.add((a, b))
+    for v in rng.choice(n, n // 3, replace=False):
+        E.add((int(v), int(v)))
+    with open(path, "w") as f:
+        for a, b in sorted(E):
+            f.write(f"{a} {b}\n")
+
+
+def _ef_bucket_edgelist(path):
+    """A hub (vertex 0) over leaves 1..3000 plus 45 vertices u_j = 3001 + j,
+    each adjacent to the hub and to 43 consecutive leaves 64(j+1)+1 ..
+    64(j+1)+43: slot (u_j -> 0) has c = 43 common neighbours in N(0)
+    (deg 3045), an Elias-Fano payload with l = 6 whose bucket j+1 holds all
+    43 of them — a run of more than 32 ones in the unary high parts."""
+    E = {(0, v) for v in range(1, 3001)}
+    for j in range(45):
+        u = 3001 + j
+        E.add((0, u))
+        for v in range(64 * (j + 1) + 1, 64 * (j + 1) + 44):
+            E.add((v, u))
+    with open(path, "w") as f:
+        for a, b in sorted(E):
+            f.write(f"{a} {b}\n")
+
+
+@pytest.mark.parametrize("mode", ["bitset", "rejection"])
+@pytest.mark.parametrize("graph", ["selfloop_sparse", "ef_bucket"])
+@pytest.mark.parametrize("p,q", [(0.25, 4), (4, 0.25)])
+def test_bitset_edge_payloads_equal_oracle(gw, oracle, tmp_path, mode, graph, p, q):
+    """Payload corner cases against the oracle: (a) return elision next to a
+    self-looped vertex (the stash is valid only when the reverse slot has no
+    common neighbour either); (b) an Elias-Fano bucket with more than 32
+    elements (membership must read past the first 32-bit window).  Both the
+    bitset kernel and the listed rejection sampler (same payloads)."""
+    import torch
+    from gwamd import _lib as C
+    path = str(tmp_path / f"{graph}.edgelist")
+    (_selfloop_sparse_edgelist if graph == "selfloop_sparse" else _ef_bucket_edgelist)(path)
+    G = gw.GWGraph.from_edgelist(path, " ", "nx").to_device(0)
+    C.check(C.lib().gw_n2v_prepare(G.handle, float(p), float(q),
+                                   C.N2V_BITSET if mode == "bitset" else C.N2V_REJECTION), G.handle)
+    n, L = G.n, 40
+    begin, count = 5, 30 * n
+    out = torch.empty((count, L), dtype=torch.int32, device="cuda")
+    lens = torch.empty(count, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    C.check(C.lib().gw_n2v_walks(G.handle, L, 9, begin, count, 1, C.ptr(out), C.ptr(lens), C.ptr(cnt), None),
+            G.handle)
+    torch.cuda.synchronize()
+    csr = G.export_csr()
+    if mode == "bitset":
+        ref, rl, rc = oracle.walks_bitset(csr, p, q, 9, L, begin, count, nthreads=8)
+    else:
+        ref, rl, rc = oracle.walks_scale(dict(csr, weights=None), p, q, 9, L, begin, count, nthreads=8)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    np.testing.assert_array_equal(lens.cpu().numpy(), rl)
+    assert int(cnt[0]) == int(rc[0]) and int(cnt[1]) == int(rc[1])
+    G.free()
+
+
 @pytest.mark.parametrize("p,q", [(1, 0.5), (0.25, 4), (1, 1)])
 def test_rejection_rmat_equals_oracle(gw, oracle, p, q):
     """Rejection sampler (slot entries + per-row neighbour hash sets) and the

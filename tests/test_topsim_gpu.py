@@ -202,3 +202,101 @@ def test_topsim_hash_overflow_rmat(gw, oracle):
         row = ref[r]
         order = sorted(np.nonzero(row > 0)[0].tolist(), key=lambda i: (-row[i], i))[:k]
         np.testing.assert_allclose(sc.cpu().numpy()[r], row[order], rtol=1e-12)
+
+
+def _sparse_gpu(g, sample, step, sources, capacity, seed=11):
+    import torch
+    from gwamd import _lib as Cl
+    g._ensure_device()
+    src = torch.as_tensor(np.asarray(sources, np.int32), device="cuda")
+    b = torch.empty(len(src), dtype=torch.int64, device="cuda")
+    ln = torch.empty(len(src), dtype=torch.int32, device="cuda")
+    ids = torch.empty(max(capacity, 1), dtype=torch.int32, device="cuda")
+    sc = torch.empty(max(capacity, 1), dtype=torch.float64, device="cuda")
+    used = torch.full((1,), 123, dtype=torch.int64, device="cuda")
+    st = torch.zeros(4, dtype=torch.int64, device="cuda")
+    h = g._g.handle
+    rc = Cl.lib().gw_topsim_sparse(h, 0, sample, step, 0.6, seed, Cl.ptr(src), len(src), capacity, Cl.ptr(b),
+                                   Cl.ptr(ln), Cl.ptr(ids), Cl.ptr(sc), Cl.ptr(used), Cl.ptr(st), None)
+    return rc, b.cpu().numpy(), ln.cpu().numpy(), ids.cpu().numpy(), sc.cpu().numpy(), int(used.cpu()[0]), \
+        st.cpu().numpy()
+
+
+def _scatter(n, b, ln, ids, sc):
+    rows = np.zeros((len(b), n))
+    for r in range(len(b)):
+        rows[r, ids[b[r]:b[r] + ln[r]]] = sc[b[r]:b[r] + ln[r]]
+    return rows
+
+
+@pytest.mark.parametrize("name,sample,step", [("moreno", 10000, 5), ("blog", 2500, 5), ("arxiv", 5000, 5)])
+def test_sparse_rows_equal_oracle_and_write_exact(gw, oracle, tmp_path, name, sample, step):
+    """gw_topsim_sparse: every nonzero entry of each row (== the oracle's rows
+    at rtol 1e-12, identical support, same counters); the capacity protocol
+    (too small -> GW_ERR_CAPACITY, *used = room needed, rows that did not fit
+    marked -1); and gw_write_sim_text_sparse on those rows byte-identical to
+    the Java-exact dense writer on the same values (Print.java:25-53)."""
+    from gwamd import _lib as Cl
+    g = _graph(gw, name)
+    n = g.getVCount()
+    sources = np.arange(n, dtype=np.int32) if n <= 1500 else np.arange(3, n, max(1, n // 500), dtype=np.int32)
+    rc, b, ln, ids, sc, used, st = _sparse_gpu(g, sample, step, sources, 1000)
+    assert rc == Cl.GW_ERR_CAPACITY and used > 1000
+    assert np.all((ln == -1) == (b == -1)) and (ln == -1).any()
+    ok = ln >= 0
+    assert int(ln[ok].sum()) <= 1000
+    rc, b, ln, ids, sc, used2, st = _sparse_gpu(g, sample, step, sources, used)
+    assert rc == 0 and used2 == used and int(ln.sum()) == used and np.all(ln >= 0)
+    rows = _scatter(n, b, ln, ids, sc)
+    ref, rst = _oracle(oracle, g, 0, sample, step, sources)
+    np.testing.assert_allclose(rows, ref, rtol=1e-12, atol=0)
+    assert np.array_equal(rows > 0, ref > 0)
+    assert st[0] == rst["extensions"] and st[1] == rst["pair_updates"] and st[3] == rst["walkers"]
+    for topk in (20, 100):
+        d, s = tmp_path / f"d{topk}", tmp_path / f"s{topk}"
+        Cl.check(Cl.lib().gw_write_sim_text_dense(str(d).encode(), Cl.ptr(rows), Cl.ptr(sources), len(sources), n,
+                                                  topk, b",", 6))
+        Cl.check(Cl.lib().gw_write_sim_text_sparse(str(s).encode(), Cl.ptr(b), Cl.ptr(ln), Cl.ptr(ids), Cl.ptr(sc),
+                                                   Cl.ptr(sources), len(sources), n, topk, b",", 6))
+        assert open(str(s) + ".sim.txt", "rb").read() == open(str(d) + ".sim.txt", "rb").read()
+        assert open(s, "rb").read() == open(d, "rb").read()
+
+
+@pytest.mark.parametrize("name,sample,step,topk", [("moreno", 1000, 5, 20), ("blog", 1000, 3, 100),
+                                                   ("arxiv", 2500, 5, 20)])
+def test_write_text_matches_java_print_on_oracle_rows(gw, oracle, tmp_path, name, sample, step, topk):
+    """gw_topsim_write_text (compute + Print.printByOrder at any V, the path
+    of config 5 and the JNI writer) against Print.printByOrder's Java
+    emulation over the oracle's rows (Java-literal summation order): min(topk,
+    V) entries per row including zero-score ids, same ids in the same order
+    except where two oracle values are equal within fp64 accumulation noise
+    (the GPU adds with atomics: rtol 1e-12), same %.6f strings except where
+    the value sits on a HALF_UP rounding boundary (C = 0.6 and integer SAMPLE
+    and degrees make exact decimal halves common, and an ulp decides them)."""
+    from gwamd import topsim
+    g = _graph(gw, name)
+    n = g.getVCount()
+    sources = np.arange(n, dtype=np.int32) if n <= 1500 else np.arange(1, n, max(1, n // 300), dtype=np.int32)
+    ts = topsim.TopSim_singleSample(g, sample, step, seed=11)
+    out = tmp_path / "w.txt"
+    ts.writeText(str(out), topk, sources=sources)
+    ref, rst = _oracle(oracle, g, 0, sample, step, sources)
+    assert ts.stats["pair_updates"] == rst["pair_updates"]
+    got = open(str(out) + ".sim.txt", "rb").read().decode().split("\r\n")
+    assert got[-1] == "" and len(got) == len(sources) + 1
+    diff_vals = 0
+    for r, v in enumerate(sources):
+        exp = oracle.java_fixed_max_pq_row(ref[r], topk)
+        toks = got[r].split(",")
+        assert toks[0] == str(v) and len(toks) - 1 == len(exp) == min(topk, n)
+        for t, (i, x) in zip(toks[1:], exp):
+            gi, gs = t.split(":")
+            if int(gi) != i:
+                assert abs(ref[r][int(gi)] - x) <= 1e-12 * max(x, 1e-300), (v, gi, i)
+            es = oracle.java_format_fixed(x)
+            if gs != es:
+                diff_vals += 1
+                assert abs(float(gs) - float(es)) <= 1.000001e-6, (v, gs, es)
+                frac = x * 1e6 - np.floor(x * 1e6)
+                assert abs(frac - 0.5) < 1e-4, (v, gs, es, x)
+    assert diff_vals <= max(2, len(sources) * topk // 1000)
