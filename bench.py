@@ -84,7 +84,8 @@ def parse(argv):
     ap.add_argument("--p", type=float, default=None)
     ap.add_argument("--q", type=float, default=None)
     ap.add_argument("--walk-length", type=int, default=80)
-    ap.add_argument("--num-walks", type=int, default=None, help="walks per node per rank per step")
+    ap.add_argument("--num-walks", type=int, default=None,
+                    help="walks per node per step: per rank (config 2, weak) or in total (config 4, strong)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--allgather", choices=["auto", "on", "off"], default="auto",
                     help="time the RCCL all-gather of the walks (auto: when ranks > 1)")
@@ -113,7 +114,7 @@ def parse(argv):
                     help="ranks + collectives with synthetic rows, no GPU work, no throughput")
     a = ap.parse_args(argv)
     cfg = {2: dict(scale=20, p=0.25, q=4.0, num_walks=10, mode="auto"),
-           4: dict(scale=24, p=1.0, q=0.5, num_walks=1, mode="rejection"),
+           4: dict(scale=24, p=1.0, q=0.5, num_walks=10, mode="rejection"),
            5: dict(scale=20, p=0.25, q=4.0, num_walks=10, mode="auto")}[a.config]
     for k, v in cfg.items():
         if getattr(a, k) is None:
@@ -332,6 +333,17 @@ class Ranks:
         else:
             self.dist.all_gather_into_tensor(out, src)
 
+    def allgather_list(self, vals):
+        """[rank][i] = every rank's list of int64 numbers."""
+        if self.world == 1:
+            return [list(vals)]
+        torch = self.torch
+        t = torch.tensor(list(vals), dtype=torch.int64, device=self.cdev)
+        out = torch.empty((self.world, len(vals)), dtype=torch.int64, device=self.cdev)
+        self.dist.all_gather_into_tensor(out, t) if self.backend == "nccl" else \
+            self.dist.all_gather(list(out.unbind(0)), t)
+        return out.tolist()
+
     def close(self):
         if self.world > 1:
             self.dist.destroy_process_group()
@@ -362,13 +374,21 @@ def time_steps(R, step, steps, warmup, stream=None, events=True):
     return el, kms
 
 
-def gather_timing(R, args, step, out, L, B):
+def gather_timing(R, args, step, out, L, B, begin_of=None, count_of=None):
     """walk + RCCL all-gather of the emitted walks per step (north_star's
     exchange), timed like the headline; rank 0 then checks the last rank's
-    gathered block against its own recomputation of that block."""
+    gathered block against its own recomputation of that block.  `out` holds
+    B rows per rank (strong shards: padded to the largest shard); rank r's
+    block of step i starts at global walk begin_of(i, r) and has count_of(r)
+    valid rows (default: weak blocks of B)."""
     torch = R.torch
+    from gwamd import dist as gdist
     row_bytes = L * 4
     world = R.world
+    if begin_of is None:
+        begin_of = lambda i, r: gdist.weak_block(i, world, r, B)  # noqa: E731
+    if count_of is None:
+        count_of = lambda r: B  # noqa: E731
     full = world * B * row_bytes <= GATHER_FULL_LIMIT
     if full:
         rows_c = B
@@ -388,22 +408,55 @@ def gather_timing(R, args, step, out, L, B):
     last = args.steps - 1
     rl = world - 1
     if R.rank == 0:
-        from gwamd import dist as gdist
-        w_last = gdist.weak_block(last, world, rl, B)
         if full:
-            got = gbuf[rl * B:(rl + 1) * B].clone()
             lo, n = 0, B
         else:
             lo = ((B - 1) // rows_c) * rows_c
             n = B - lo
-            got = gbuf[rl * n:(rl + 1) * n].clone()
-        mine = step.recompute(w_last + lo, n)
-        check = bool(torch.equal(got.cpu(), mine.cpu()))
+        got = gbuf[rl * n:(rl + 1) * n].clone()
+        nv = max(0, min(n, count_of(rl) - lo))  # valid (non-padding) rows of that block
+        mine = step.recompute(begin_of(last, rl) + lo, nv)
+        check = bool(torch.equal(got[:nv].cpu(), mine.cpu()))
     ok = R.allreduce([1.0 if (check is None or check) else 0.0], "max")
     return {"seconds": el, "ms_per_step": el / args.steps * 1e3,
             "gathered_bytes_per_step_per_rank": (world - 1) * B * row_bytes,
             "mode": "whole" if full else f"ring of {rows_c}-row chunks",
             "check_last_rank_block_identical": check}, ok
+
+
+def checksum(t):
+    """Position-weighted checksum of a tensor's bytes (int64, device-side)."""
+    import torch
+    v = t.contiguous().view(torch.int32).reshape(-1).to(torch.int64)
+    w = torch.arange(v.numel(), dtype=torch.int64, device=v.device) % 65521 + 1
+    return int((v * w).sum().item())
+
+
+def gather_rows_timing(R, args, tensors, run=None):
+    """All-gather of per-rank row blocks (same row count on every rank:
+    strong shards padded), timed over args.steps, each step optionally
+    preceded by `run()`; every rank's received blocks are checked against
+    the senders' checksums (all-gathered beforehand)."""
+    torch = R.torch
+    world = R.world
+    bufs = [torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=R.dev) for t in tensors]
+
+    def gstep(i, ev):
+        if run is not None:
+            run()
+        for t, g in zip(tensors, bufs):
+            R.allgather_into(g, t)
+    el, _ = time_steps(R, gstep, args.steps, 0, events=False)
+    mine = [checksum(t) for t in tensors]
+    sums = R.allgather_list(mine)  # [rank][tensor]
+    ok = all(checksum(g[r * t.shape[0]:(r + 1) * t.shape[0]]) == sums[r][k]
+             for k, (t, g) in enumerate(zip(tensors, bufs)) for r in range(world))
+    allok = R.allreduce([0.0 if ok else 1.0], "max")[0] == 0.0
+    nbytes = sum(t.numel() * t.element_size() for t in tensors)
+    return {"seconds": el, "ms_per_step": el / args.steps * 1e3,
+            "gathered_bytes_per_step_per_rank": (world - 1) * nbytes,
+            "xgmi_GBps_per_rank": (world - 1) * nbytes * args.steps / el / 1e9,
+            "check_blocks_match_sender_checksums": bool(allok)}
 
 
 # ---- workloads -----------------------------------------------------------------
@@ -435,23 +488,36 @@ def walk_headline(R, args):
     L = args.walk_length
     world, rank = R.world, R.rank
 
+    strong = args.config == 4  # BASELINE config 4: the r=10 workload split over the ranks
+
+    def shape(n):
+        """(rows per rank buffer, this rank's first walk of step i, valid rows per rank)."""
+        if strong:
+            total = args.num_walks * n
+            b0, cnt = gdist.shard_range(total, world, rank)
+            rows = -(-total // world)
+            return rows, (lambda i: b0), cnt, total, \
+                (lambda i, r: gdist.shard_range(total, world, r)[0]), (lambda r: gdist.shard_range(total, world, r)[1])
+        B = args.num_walks * n
+        return B, (lambda i: gdist.weak_block(i, world, rank, B)), B, B * world, None, None
+
     if R.plumbing:
         n = 1 << args.scale
-        B = args.num_walks * n
-        out = torch.empty((B, L), dtype=torch.int32)
+        B, first, cnt_w, total, begin_of, count_of = shape(n)
+        out = torch.full((B, L), -1, dtype=torch.int32)
 
         def synth(w0, cnt):  # NOT walks: row w = (w*L + t) mod 2^31, for the rank/collective plumbing only
             w = torch.arange(w0, w0 + cnt, dtype=torch.int64).unsqueeze(1)
             return ((w * L + torch.arange(L, dtype=torch.int64)) % (2**31 - 1)).to(torch.int32)
         def step(i, ev):
-            out.copy_(synth(gdist.weak_block(i, world, rank, B), B))
+            out[:cnt_w].copy_(synth(first(i), cnt_w))
         step.recompute = synth
         el, _ = time_steps(R, step, args.steps, args.warmup, events=False)
-        steps_total = int(R.allreduce([args.steps * B * (L - 1)], "sum", torch.int64)[0])
+        steps_total = int(R.allreduce([args.steps * cnt_w * (L - 1)], "sum", torch.int64)[0])
         res = {"value": None, "walk_steps": steps_total, "seconds": el, "n": n, "nnz": None, "mode": "plumbing",
-               "B": B}
+               "B": B, "walks_per_step": total}
         if world > 1 and args.allgather != "off":
-            g, ok = gather_timing(R, args, step, out, L, B)
+            g, ok = gather_timing(R, args, step, out, L, B, begin_of, count_of)
             res["allgather"] = g
             res["allgather_all_ranks_ok"] = bool(ok[0] >= 1.0)
         return res
@@ -466,6 +532,9 @@ def walk_headline(R, args):
     log(f"[rank {rank}] rmat-{args.scale} ef {args.edge_factor}: n={n} nnz={nnz} maxdeg={inf.max_degree} "
         f"built in {time.perf_counter() - t0:.1f}s")
     G.to_device(R.dev.index)
+    # the sampler tables are chosen for this rank's share of one BASELINE
+    # workload pass (r walks from every vertex)
+    G.options(expected_steps=shape(n)[2] * (L - 1))
     t0 = time.perf_counter()
     mode = "bitset" if args.mode in ("auto", "bitset") else "rejection"
     if args.p == 1.0 and args.q == 1.0:
@@ -487,8 +556,10 @@ def walk_headline(R, args):
         mode = "first-order"
     log(f"[rank {rank}] prepare ({mode}) {prep_s:.2f}s, sampler tables {sampler_bytes / 1e9:.2f} GB")
 
-    B = args.num_walks * n  # walks per rank per step
+    B, first, cnt_w, total, begin_of, count_of = shape(n)  # buffer rows per rank, shard start, valid rows
     out = torch.empty((B, L), dtype=torch.int32, device=R.dev)
+    if cnt_w < B:
+        out[cnt_w:].fill_(-1)  # padding row of a short strong shard (gathered, never walked)
     cnt = torch.zeros(2, dtype=torch.int64, device=R.dev)
     stream = torch.cuda.current_stream(R.dev)
     sh = C.ctypes.c_void_p(stream.cuda_stream)
@@ -498,11 +569,12 @@ def walk_headline(R, args):
                                      C.ptr(counters) if counters is not None else None, sh), G.handle)
 
     def step(i, ev):
-        # global walk-index block of (rank, step i): iterations num_walks*(i*world+rank) ...
-        w0 = gdist.weak_block(i, world, rank, B)
+        # global walk-index block of (rank, step i): weak, iterations
+        # num_walks*(i*world+rank) ...; strong, this rank's shard of the r=10 workload
+        w0 = first(i)
         if ev is not None:
             ev[0].record(stream)
-        launch(w0, B, out, cnt)
+        launch(w0, cnt_w, out, cnt)
         if ev is not None:
             ev[1].record(stream)
 
@@ -521,7 +593,7 @@ def walk_headline(R, args):
     steps_local, trials_local = int(cnt[0].item()), int(cnt[1].item())
     steps_total, trials_total = (int(x) for x in R.allreduce([steps_local, trials_local], "sum", torch.int64))
     value = steps_total / el
-    launch_steps = steps_local // args.steps
+    launch_steps = steps_local // args.steps  # this rank's launch
     achieved = BYTES_PER_STEP * launch_steps / (k_avg_ms * 1e-3) / 1e9
     kname = walk_kernel_name(mode, G)
     tag = f"n2v_rmat{args.scale}_ef{args.edge_factor}_p{args.p}_q{args.q}_L{L}_r{args.num_walks}_{mode}"
@@ -552,7 +624,10 @@ def walk_headline(R, args):
             sys.exit(3)
 
     res = {"value": value, "walk_steps": steps_total, "seconds": el, "n": n, "nnz": nnz, "mode": mode,
-           "B": B, "prep_s": prep_s, "sampler_gb": sampler_bytes / 1e9,
+           "B": B, "walks_per_step": total, "prep_s": prep_s, "sampler_gb": sampler_bytes / 1e9,
+           "end_to_end": end_to_end(prep_s, el / args.steps, steps_total // args.steps, 1.0,
+                                    "prepare + one step (the BASELINE workload: every vertex starts "
+                                    f"{args.num_walks} walks of length {L})"),
            "trials_per_step": trials_total / max(steps_total, 1),
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -562,7 +637,7 @@ def walk_headline(R, args):
                         "bytes_per_unit": BYTES_PER_STEP, "units_per_launch": launch_steps,
                         "lib_sha256": lib_digest(), "random_line_roofline": line_rate}}
     if world > 1 and args.allgather != "off":
-        g, ok = gather_timing(R, args, step, out, L, B)
+        g, ok = gather_timing(R, args, step, out, L, B, begin_of, count_of)
         g["value"] = steps_total / g["seconds"]
         g["unit"] = "walk-steps/s (walks all-gathered to every rank)"
         g["xgmi_GBps_per_rank"] = g["gathered_bytes_per_step_per_rank"] * args.steps / g["seconds"] / 1e9
@@ -577,6 +652,16 @@ def walk_headline(R, args):
     return res
 
 
+def end_to_end(prep_s, launch_s, launch_steps, launches, what):
+    """Prepare (preprocess_transition_probs' replacement) plus every walk of
+    the BASELINE workload: `launches` launches of `launch_s` seconds
+    (measured; scaled when the timed launch is a fraction of the workload)."""
+    walk_s = launch_s * launches
+    return {"prepare_s": prep_s, "walk_s": walk_s, "total_s": prep_s + walk_s,
+            "walk_steps": int(launch_steps * launches), "value": launch_steps * launches / (prep_s + walk_s),
+            "unit": "walk-steps/s", "prepare_share": prep_s / (prep_s + walk_s), "workload": what}
+
+
 def walk_kernel_name(mode, G):
     """The kernel a prepared graph's walks launch: the bitset sampler, the
     listed rejection sampler (64 B slot entries, built for unweighted
@@ -589,8 +674,14 @@ def walk_kernel_name(mode, G):
     return "k_walk_scale"
 
 
-def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejection=False, walks_per_node=1):
-    """One launch of `walks_per_node` walks per node per rank on graph BG (weak)."""
+def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejection=False, walks_per_node=1,
+                   strong_walks=None, baseline_r=10):
+    """One launch on graph BG: `walks_per_node` walks per node per rank (weak),
+    or, with strong_walks = r, the fixed workload of r walks per node split
+    over the ranks (BASELINE config 4: strong scaling) followed at ranks > 1 by
+    the timed RCCL all-gather of every walk into every rank.  end_to_end =
+    prepare + all walks of the BASELINE workload (r = baseline_r walks per
+    node; a 1-walk launch is scaled by r)."""
     torch = R.torch
     import gwamd  # noqa: F401
     from gwamd import _lib as C
@@ -611,20 +702,42 @@ def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejectio
     if wp == 1.0 and wq == 1.0:
         bmode = "first-order"  # k_walk_scale<true,...>: no per-edge tables
     bprep = time.perf_counter() - t0
-    nb = int(bi.n) * walks_per_node
-    bout = torch.empty((nb, L), dtype=torch.int32, device=R.dev)
+    if strong_walks:
+        total = int(bi.n) * strong_walks
+        b0, nb = gdist.shard_range(total, world, rank)
+        rows = -(-total // world)
+        first = lambda i: b0  # noqa: E731
+        begin_of = lambda i, r: gdist.shard_range(total, world, r)[0]  # noqa: E731
+        count_of = lambda r: gdist.shard_range(total, world, r)[1]  # noqa: E731
+    else:
+        nb = rows = int(bi.n) * walks_per_node
+        total = nb * world
+        first = lambda i: gdist.weak_block(i, world, rank, nb)  # noqa: E731
+        begin_of = count_of = None
+    bout = torch.empty((rows, L), dtype=torch.int32, device=R.dev)
+    if nb < rows:
+        bout[nb:].fill_(-1)
     bcnt = torch.zeros(2, dtype=torch.int64, device=R.dev)
     stream = torch.cuda.current_stream(R.dev)
     sh = C.ctypes.c_void_p(stream.cuda_stream)
 
+    def launch(w0, count, dst, counters):
+        C.check(C.lib().gw_n2v_walks(BG.handle, L, args.seed, w0, count, 1, C.ptr(dst), None,
+                                     C.ptr(counters) if counters is not None else None, sh), BG.handle)
+
     def bstep(i, ev):
-        w0 = gdist.weak_block(i, world, rank, nb)
         if ev is not None:
             ev[0].record(stream)
-        C.check(C.lib().gw_n2v_walks(BG.handle, L, args.seed, w0, nb, 1, C.ptr(bout), None, C.ptr(bcnt), sh),
-                BG.handle)
+        launch(first(i), nb, bout, bcnt)
         if ev is not None:
             ev[1].record(stream)
+
+    def recompute(w0, count):
+        dst = torch.empty((count, L), dtype=torch.int32, device=R.dev)
+        launch(w0, count, dst, None)
+        torch.cuda.synchronize()
+        return dst
+    bstep.recompute = recompute
 
     bstep(0, None)
     torch.cuda.synchronize()
@@ -632,21 +745,40 @@ def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejectio
     sec, kms = time_steps(R, lambda i, ev: bstep(1 + i, ev), 1, 0)
     bsteps = int(R.allreduce([int(bcnt[0].item())], "sum", torch.int64)[0])
     local_steps = int(bcnt[0].item())
+    gather = None
+    if world > 1 and strong_walks and args.allgather != "off":
+        ga = argparse.Namespace(**vars(args))
+        ga.steps = 1
+        g, ok = gather_timing(R, ga, lambda i, ev: bstep(1 + i, ev), bout, L, rows,
+                              lambda i, r: begin_of(i, r), count_of)
+        g["value"] = bsteps / g["seconds"]
+        g["unit"] = "walk-steps/s (walks all-gathered to every rank)"
+        g["xgmi_GBps_per_rank"] = g["gathered_bytes_per_step_per_rank"] / g["seconds"] / 1e9
+        g["all_ranks_ok"] = bool(ok[0] >= 1.0)
+        gather = g
     cpu_b = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu_b = cpu_baseline_walks(BG.export_csr(), wp, wq, args.seed, L, 0, 10.0, max_walks=2_000_000)
     del bout
     kname = walk_kernel_name(bmode, BG)
-    tag = f"n2v_rmat{scale}_ef{ef}_p{wp}_q{wq}_L{L}_r{walks_per_node}_{bmode}"
+    rtag = strong_walks if strong_walks else walks_per_node
+    tag = f"n2v_rmat{scale}_ef{ef}_p{wp}_q{wq}_L{L}_r{rtag}_{bmode}" + (f"_of{world}" if strong_walks and world > 1
+                                                                         else "")
     prof = load_prof(tag, local_steps)
     sbytes = BG.info().sampler_bytes
     line = line_roofline(prof, kms * 1e-3, sbytes if bmode == "bitset" else max(sbytes, 16 * bi.nnz))
+    r_run = strong_walks if strong_walks else walks_per_node * world
+    e2e = end_to_end(bprep, sec, bsteps, baseline_r / r_run,
+                     f"prepare + {baseline_r} walks from every vertex (BASELINE workload)" +
+                     ("" if r_run == baseline_r else f"; the timed launch ran {r_run}, scaled"))
     return {"metric": f"walk-steps/sec (node2vec, {what})", "value": bsteps / sec, "unit": "walk-steps/s",
-            "n_ranks": world, "scaling": "weak",
+            "n_ranks": world, "scaling": "strong" if strong_walks else "weak",
             "config": {"workload": f"node2vec p={wp} q={wq} on Graph500 R-MAT scale-{scale} ef {ef} "
-                                   f"(n={bi.n}, adjacency entries={bi.nnz}), walk_length={L}, "
-                                   f"{walks_per_node} walk(s)/node per rank", "sampler": bmode},
-            "kernel_ms": kms,
+                                   f"(n={bi.n}, adjacency entries={bi.nnz}), walk_length={L}, " +
+                                   (f"{strong_walks} walks/node in total split over {world} rank(s)" if strong_walks
+                                    else f"{walks_per_node} walk(s)/node per rank"),
+                       "sampler": bmode, "walks": total},
+            "kernel_ms": kms, "walk_steps": bsteps,
             "roofline": {"bound": "hbm", "achieved": BYTES_PER_STEP * local_steps / (kms * 1e-3) / 1e9,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": BYTES_PER_STEP * local_steps / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -655,7 +787,7 @@ def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejectio
                          "pmc_match": {"kernel": kname, "grid": grid_threads(nb)},
                          "random_line_roofline": line},
             "host_build_s": build_s, "prepare_s": bprep, "sampler_tables_gb": BG.info().sampler_bytes / 1e9,
-            "cpu_baseline": cpu_b}
+            "end_to_end": e2e, "allgather": gather, "cpu_baseline": cpu_b}
 
 
 TOPSIM_GRAPHS = {"blog": ("blog.txt", 10313, ",", "lshrank blog, V=10313, 333,983 edges"),
@@ -701,6 +833,23 @@ def run_topsim(R, args, name):
     world, rank = R.world, R.rank
     K, sample, step = 20, args.topsim_sample, args.topsim_step
     offs = nbrs = None
+    if R.plumbing:  # config 5's rank / collective path with synthetic rows (no GPU)
+        K, nsrc_all = 100, 1 << args.scale
+        srcs = np.arange(nsrc_all, dtype=np.int32)[rank::world]
+        rows = -(-nsrc_all // world)
+        ids = torch.full((rows, K), -1, dtype=torch.int32)
+        sc = torch.zeros((rows, K), dtype=torch.float64)
+
+        def synth():
+            s_ = torch.as_tensor(srcs, dtype=torch.int64).unsqueeze(1)
+            ids[:len(srcs)] = ((s_ * K + torch.arange(K)) % nsrc_all).to(torch.int32)
+            sc[:len(srcs)] = s_.to(torch.float64) + torch.arange(K, dtype=torch.float64) / K
+        synth()
+        g = gather_rows_timing(R, args, [ids, sc], run=synth) if world > 1 else None
+        return {"metric": "SimRank pair-updates/sec (TopSim_singleSample)", "value": None, "unit": "pair-updates/s",
+                "n_ranks": world, "scaling": "strong", "seconds": g["seconds"] if g else 0.0,
+                "config": {"workload": f"plumbing: {nsrc_all} synthetic top-{K} rows split round-robin",
+                           "topk": K}, "pair_updates": 0, "cpu_baseline": None, "roofline": None, "allgather": g}
     if name == "p10m":
         # config 5: 10M-vertex Java-semantics R-MAT (reference quadrant recursion),
         # 1e8 generated lines, all non-isolated sources, top-100
@@ -756,6 +905,28 @@ def run_topsim(R, args, name):
             ev[1].record(stream)
     tel, kms = time_steps(R, tstep, 1, 0)
     ext_l, upd_l = int(st[0].item()), int(st[1].item())
+    gather = None
+    if name == "p10m" and world > 1 and args.allgather != "off":
+        # every rank receives all top-k rows (k x (int32 + fp64)
+        # per source; round-robin shards padded to the longest)
+        rows = -(-len(srcs_all) // world)
+        gid = torch.full((rows, K), -1, dtype=torch.int32, device=R.dev)
+        gsc = torch.zeros((rows, K), dtype=torch.float64, device=R.dev)
+        gid[:nloc].copy_(ids[:nloc])
+        gsc[:nloc].copy_(sc[:nloc])
+        ga = argparse.Namespace(**vars(args))
+        ga.steps = 1
+        gonly = gather_rows_timing(R, ga, [gid, gsc])
+
+        def both():
+            ts_run(None)
+            gid[:nloc].copy_(ids[:nloc])
+            gsc[:nloc].copy_(sc[:nloc])
+        gboth = gather_rows_timing(R, ga, [gid, gsc], run=both)
+        gather = dict(gboth, allgather_only_s=gonly["seconds"], rows_per_rank=rows,
+                      value=upd / gboth["seconds"], unit="pair-updates/s (top-k rows all-gathered to every rank)",
+                      check_blocks_match_sender_checksums=gonly["check_blocks_match_sender_checksums"] and
+                      gboth["check_blocks_match_sender_checksums"])
     ext, upd = (int(x) for x in R.allreduce([ext_l, upd_l], "sum", torch.int64))
     tag = f"topsim_{name}_s{sample}_t{step}_k{K}"
     cpu_ts = None
@@ -768,7 +939,7 @@ def run_topsim(R, args, name):
         "unit": "pair-updates/s", "path_extensions_per_s": ext / tel, "n_ranks": world, "scaling": scaling,
         "config": {"workload": f"TopSim_singleSample on {name} ({desc}, Java multigraph)",
                    "step": step, "sample": sample, "C": 0.6, "topk": K},
-        "pair_updates": upd, "path_extensions": ext, "seconds": tel, "cpu_baseline": cpu_ts,
+        "pair_updates": upd, "path_extensions": ext, "seconds": tel, "cpu_baseline": cpu_ts, "allgather": gather,
         "roofline": topsim_roofline(ext_l, upd_l, kms * 1e-3, tag, nloc, int(offs[-1]), step),
     }
 
@@ -891,8 +1062,6 @@ def main(argv):
     secondary = {}
     cpu = None
     if args.config == 5:
-        if R.plumbing:
-            raise SystemExit("--plumbing-check covers configs 2 and 4")
         h = run_topsim(R, args, "p10m")
         value, metric, unit = h["value"], h["metric"], h["unit"]
         head = h
@@ -932,8 +1101,10 @@ def main(argv):
             BG = gwamd_graph_rmat(24, 16, a, b, c, args.seed)
             build_s = time.perf_counter() - t0
             BG.to_device(R.dev.index)
+            BG.options(expected_steps=10 * BG.n * (args.walk_length - 1))  # the sampler is chosen for r=10
             secondary["walk_rmat24_p1q05"] = walk_secondary(R, args, BG, build_s, 1.0, 0.5, 24, 16,
-                                                            "config 4 R-MAT-24 ef 16", force_rejection=True)
+                                                            "config 4 R-MAT-24 ef 16", force_rejection=True,
+                                                            strong_walks=10)
             BG.free()
         if not args.no_p10m:
             secondary["topsim_p10m"] = run_topsim(R, args, "p10m")
@@ -949,7 +1120,7 @@ def main(argv):
             "warmup": args.warmup if args.config != 5 else 1,
             "ms_per_step": head["seconds"] / (args.steps if args.config != 5 else 1) * 1e3,
             "higher_is_better": True,
-            "scaling": "weak" if args.config != 5 else "strong",
+            "scaling": "weak" if args.config == 2 else "strong",
             "vs_baseline": None,
             "dtype": "int32 ids / f64 accept tests" if args.config != 5 else "f64 scores / int32 ids",
             "data": "synthetic" if not R.plumbing else "plumbing-check: synthetic rows, no GPU work",
@@ -962,21 +1133,25 @@ def main(argv):
             res["roofline"] = head["roofline"]
             res["cpu_baseline"] = head["cpu_baseline"]
             res["pair_updates"] = head["pair_updates"]
+            if head.get("allgather"):
+                res["allgather"] = head["allgather"]
         else:
             a, b, c = rmat_abc(args)
             res["config"] = {
                 "workload": f"node2vec p={args.p} q={args.q} on synthetic R-MAT scale-{args.scale} (ef "
                             f"{args.edge_factor}, a,b,c={a},{b},{c}, seed {args.seed}; n={head['n']}, "
                             f"adjacency entries={head['nnz']}), walk_length={args.walk_length}, "
-                            f"{args.num_walks} walks/node per rank per step",
+                            f"{args.num_walks} walks/node " + ("per step in total (split over the ranks)"
+                                                               if args.config == 4 else "per rank per step"),
                 "baseline_config": args.config,
-                "walks_per_step": head["B"] * R.world, "walk_length": args.walk_length,
-                "parallelism": f"replicated graph, walks sharded over {R.world} rank(s)"}
+                "walks_per_step": head["walks_per_step"], "walk_length": args.walk_length,
+                "parallelism": f"replicated graph, walks sharded over {R.world} rank(s)" +
+                               (" (the fixed r-walk workload split: strong scaling)" if args.config == 4 else "")}
             res["walk_steps"] = head["walk_steps"]
-            for k in ("mode", "prep_s", "sampler_gb", "trials_per_step"):
+            for k in ("mode", "prep_s", "sampler_gb", "trials_per_step", "end_to_end"):
                 if k in head:
                     res[{"mode": "sampler", "prep_s": "prepare_seconds", "sampler_gb": "sampler_tables_gb",
-                         "trials_per_step": "rejection_trials_per_step"}[k]] = head[k]
+                         "trials_per_step": "rejection_trials_per_step", "end_to_end": "end_to_end"}[k]] = head[k]
             res["roofline"] = head.get("roofline")
             res["cpu_baseline"] = cpu
             if res["roofline"] is not None and R.rank == 0:

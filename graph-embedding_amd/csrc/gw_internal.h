@@ -135,6 +135,7 @@ struct gw_ts_sparse {
 };
 
 struct gw_graph {
+  gw_options_t opt{0, 0, -1, 0, 0};  // per-handle tuning (gw_graph_set_options)
   // host CSR
   int semantics = 0;
   int directed = 0;
@@ -223,6 +224,7 @@ int gw_dev_topsim_m(gw_graph* g, int variant, int capacity, int sample, int step
                     int32_t* out_size_dev, int64_t* stats_dev, void* stream);
 int gw_dev_simrank_naive(gw_graph* g, double C, int iters, double* sim_dev, void* stream);
 int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only = false);
+double gw_bitset_build_model_s(gw_graph* g);
 int gw_dev_walk_bitset_launch(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int64_t walk_count,
                               int shuffle, int32_t* out_dev, int32_t* len_dev, uint64_t* counters_dev,
                               void* stream);

@@ -583,6 +583,27 @@ int gw_dev_upload(gw_graph* g, int device) {
   return GW_OK;
 }
 
+// per-slot sampler tables may take this much HBM (the handle's option, else
+// half of the free HBM)
+static int64_t table_budget(gw_graph* g) {
+  size_t fr = 0, tot = 0;
+  int64_t budget = hipMemGetInfo(&fr, &tot) == hipSuccess ? (int64_t)(fr / 2) : 0;
+  if (g->opt.table_budget_bytes > 0) budget = std::min(budget, g->opt.table_budget_bytes);
+  return budget;
+}
+
+// GW_N2V_REJECTION on an unweighted undirected graph: build the 64 B listed
+// entries?  They save ~0.46 fabric requests per second-order step (config 4:
+// 1.60 -> 1.14 requests/step at ~4.9e10 requests/s) but cost an
+// edge-centric common-neighbour build; with expected_steps known, build them
+// only when the modelled build time is paid back.
+static bool listed_pays(gw_graph* g) {
+  if (g->opt.listed == 0) return false;
+  if (g->opt.listed == 1 || g->opt.expected_steps <= 0) return true;
+  const double save_s = (double)g->opt.expected_steps * (0.46 / 4.9e10);
+  return save_s > gw_bitset_build_model_s(g);
+}
+
 int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
   if (g->device < 0) {
     g->err = "graph is not on a device (call gw_graph_to_device)";
@@ -663,8 +684,9 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
       }
     }
   }
-  if ((mode == GW_N2V_BITSET || (mode == GW_N2V_REJECTION && !(p == 1.0 && q == 1.0) && !d.eh)) && g->nnz &&
-      !(nobm && nobm[0] == '1')) {
+  // membership pre-filter for has_edge probes of the rejection sampler when
+  // the exact hash does not fit (the bitset build intersects rows directly)
+  if (mode == GW_N2V_REJECTION && !(p == 1.0 && q == 1.0) && !d.eh && g->nnz && !(nobm && nobm[0] == '1')) {
     const int64_t words = (16 * g->nnz + 31) / 32 + 1;
     if ((rc = dev_alloc(g, &d.bitmap, words))) return rc;
     GW_HIP_TRY(hipMemset(d.bitmap, 0, sizeof(uint32_t) * words));
@@ -680,11 +702,8 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
   // HBM, < 2^32 slots) the 16 B slot entries below serve k_walk_scale
   bool listed = false;
   if (mode == GW_N2V_REJECTION && !fo && g->nnz && !g->weighted && !g->directed &&
-      g->semantics == GW_SEM_NX_SIMPLE && !GW_DIAG_ENV("GW_DIAG_NO_LISTS")) {
-    size_t fr = 0, tot = 0;
-    int64_t budget = 0;
-    if (hipMemGetInfo(&fr, &tot) == hipSuccess) budget = (int64_t)(fr / 2);
-    rc = gw_dev_bitset_build(g, budget, true);
+      g->semantics == GW_SEM_NX_SIMPLE && !GW_DIAG_ENV("GW_DIAG_NO_LISTS") && listed_pays(g)) {
+    rc = gw_dev_bitset_build(g, table_budget(g), true);
     if (rc == GW_OK) {
       listed = true;
     } else if (rc == GW_ERR_CAPACITY || rc == GW_ERR_NOMEM) {
@@ -699,13 +718,9 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
   if ((mode == GW_N2V_REJECTION || fo) && !listed && g->nnz && !(nosent && nosent[0] == '1')) {
     // slot entries (16 B per slot, one dwordx4 per step) spare the candidate's
     // offsets[] read: +14% on R-MAT-24 ef 16 (p=1, q=0.5; 8.3 GB of entries),
-    // so they are built whenever they fit in half of the free HBM
-    // (GW_SENT_MAX_GB caps them, an A/B knob).
-    size_t fr = 0, tot = 0;
+    // so they are built whenever they fit the table budget
     const int64_t ent_bytes = g->nnz * (int64_t)sizeof(gw_ts_ent);
-    int64_t ent_max = INT64_MAX;
-    if (const char* sm = getenv("GW_SENT_MAX_GB")) ent_max = (int64_t)(atof(sm) * (double)(1 << 30));
-    if (ent_bytes <= ent_max && hipMemGetInfo(&fr, &tot) == hipSuccess && (int64_t)fr / 2 > ent_bytes) {
+    if (ent_bytes <= table_budget(g)) {
       if (dev_alloc(g, &d.sent, g->nnz) == GW_OK) {
         k_scale_ent<<<grid_for(g->nnz), kBlock>>>(d, d.sent);
         GW_HIP_TRY(hipGetLastError());
@@ -717,13 +732,7 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
     }
   }
   if (mode == GW_N2V_BITSET && !(p == 1.0 && q == 1.0)) {
-    // budget: half of the free HBM (GW_BITSET_BUDGET_GB lowers it)
-    size_t fr = 0, tot = 0;
-    int64_t budget = (int64_t)64 << 30;
-    if (hipMemGetInfo(&fr, &tot) == hipSuccess) budget = (int64_t)(fr / 2);
-    if (const char* bb = getenv("GW_BITSET_BUDGET_GB"))
-      budget = std::min<int64_t>(budget, (int64_t)(atof(bb) * (double)(1 << 30)));
-    if ((rc = gw_dev_bitset_build(g, budget))) return rc;
+    if ((rc = gw_dev_bitset_build(g, table_budget(g)))) return rc;
   }
   g->p = p;
   g->q = q;
@@ -864,6 +873,18 @@ int gw_dev_n2v_walks(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int6
                      int shuffle, int32_t* out_dev, int32_t* len_dev, uint64_t* counters_dev,
                      void* stream) {
   if (walk_count <= 0) return GW_OK;
+  // one thread per walk and a launch's work-items must stay below 2^32:
+  // split larger requests (walks are a pure function of the global index)
+  constexpr int64_t kMaxLaunch = (int64_t)1 << 31;
+  if (walk_count > kMaxLaunch) {
+    for (int64_t o = 0; o < walk_count; o += kMaxLaunch) {
+      const int rc = gw_dev_n2v_walks(g, L, seed, walk_begin + o, std::min(kMaxLaunch, walk_count - o), shuffle,
+                                      out_dev + o * (int64_t)L, len_dev ? len_dev + o : nullptr, counters_dev,
+                                      stream);
+      if (rc != GW_OK) return rc;
+    }
+    return GW_OK;
+  }
   const bool first_order = (g->p == 1.0 && g->q == 1.0);
   if (!first_order && g->semantics != GW_SEM_NX_SIMPLE) {
     g->err = "second-order walks need sorted rows (NX_SIMPLE semantics)";
@@ -961,8 +982,7 @@ extern "C" int gw_n2v_walks_host(gw_graph* g, int walk_len, uint64_t seed, int64
   // Chunks of ~256 MB of walks, double-buffered: chunk k+1 is walked on one
   // stream while chunk k is copied out on another (a pageable copy blocks
   // the host, so the next kernel is enqueued before it).
-  int64_t chunk_bytes = (int64_t)256 << 20;
-  if (const char* cm = getenv("GW_HOST_CHUNK_MB")) chunk_bytes = std::max<int64_t>(1, atoll(cm)) << 20;
+  const int64_t chunk_bytes = g->opt.host_chunk_bytes > 0 ? g->opt.host_chunk_bytes : (int64_t)256 << 20;
   const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(walk_count, chunk_bytes / (4 * (int64_t)walk_len)));
   const int64_t nch = (walk_count + chunk - 1) / chunk;
   int32_t *d_out[2] = {nullptr, nullptr}, *d_len[2] = {nullptr, nullptr};

@@ -55,7 +55,6 @@ namespace {
 constexpr int kB = 256;
 constexpr int kBlk = 16;         // words per 512-bit block: regions, directory and bits are block-aligned
 constexpr int kDirBits = 512;    // bits per directory block
-constexpr int kSmallD = 32;      // thread-per-slot fill up to this degree
 constexpr int kStage = 16;
 
 constexpr int kPDir = 8;         // region entries with <= this many directory blocks keep the directory in the entry
@@ -68,18 +67,6 @@ __host__ __device__ __forceinline__ int64_t bs_boff(int64_t d) {
 }
 __host__ __device__ __forceinline__ int64_t bs_words(int64_t d) {
   return gw_bs_is_inline((uint32_t)d) ? 0 : bs_boff(d) + bs_round((d + 31) / 32);
-}
-
-__device__ __forceinline__ int32_t row_of_slot(const int64_t* __restrict__ off, int64_t n, int64_t e) {
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    int64_t mid = (lo + hi) >> 1;
-    if (off[mid + 1] <= e)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  return (int32_t)lo;
 }
 
 __device__ __forceinline__ bool bs_has_edge(const gw_dev_graph& G, int64_t rb, int64_t re, int32_t key) {
@@ -115,12 +102,23 @@ __device__ __forceinline__ int word_select(uint32_t x, uint32_t j) {
 }
 
 // ---- build ------------------------------------------------------------------
-// Common neighbours of slot (u -> v) are enumerated from the SHORTER of the two
-// sorted rows: over N(v) with has_edge(u, x) probes, or over N(u) with a
-// search in N(v) (the search window only moves forward, rows being sorted).
-// Either way positions k in N(v) come out ascending, so cost is
-// min(deg u, deg v) probes per slot instead of deg(v).
-constexpr int kThreadMin = 64;  // slots whose shorter row is <= this: one thread, else one wave
+// Edge-centric common-neighbour enumeration (k_bs_tri).  Every undirected edge
+// {u, v} is handled once, by its higher-degree end u (equal degrees: the
+// smaller id).  A workgroup holds N(u) in an LDS hash (id -> position in N(u);
+// hubs in chunks of kTriH ids, each chunk an id range), and one wave per edge
+// streams N(v) through it — coalesced, 64 elements a round.  A hit x at index
+// k of N(v) and position pu of N(u) is a common neighbour of BOTH directed
+// slots of the edge:
+//   (u -> v): position k in N(v), unless x == u;   (v -> u): position pu in N(u), unless x == v,
+// and since both rows are sorted by id, the positions of both slots come out
+// ascending.  The same stream finds kp(u -> v) (x == u at index k) and with it
+// the reverse slot offsets[v] + k; kp(v -> u) is the edge's index j in N(u).
+// Work: sum over edges of min(deg u, deg v) LDS probes plus one coalesced read
+// of the shorter row (R-MAT-20: 6.9e9) — the per-slot build this replaces
+// probed min(deg) for each DIRECTED slot with binary searches in HBM, twice.
+// Pass 1 (COUNT) writes both entries' headers (x, deg, offsets, meta, kp, c);
+// pass 2 (FILL), after the region layout, replays the stream and writes the
+// payloads through BsEmit (common positions in ascending order with ranks).
 
 enum { BS_LIST = 0, BS_INLINE = 1, BS_EF = 2, BS_REGION = 3 };
 constexpr uint32_t kFiltL = 320;  // lists-only builds: a region-size common set leaves a 320-bucket draw filter
@@ -159,109 +157,10 @@ __device__ __forceinline__ uint32_t bs_meta(uint32_t c, uint32_t d) {
   const uint32_t bblk = (mode == BS_REGION) ? (uint32_t)(bs_boff(d) / kBlk) : 0u;
   return mode | (l << 2) | (U << 7) | (bblk << 16);
 }
-// meta of slot (u -> x) with c common neighbours (u's row is [ub, ue))
-__device__ __forceinline__ uint32_t bs_meta_slot(const gw_dev_graph& G, uint32_t c, uint32_t d, int32_t u, int64_t ub,
-                                                 int64_t ue) {
-  if (c == 0u && d < GW_BS_PACK_D && gw_row_find(G.nbrs, ub, ue, u) < 0) return kMetaStashOk;  // list mode, meta 0
+// meta of slot (u -> x) with c common neighbours; u_loop: u has a self-loop
+__device__ __forceinline__ uint32_t bs_meta_slot(uint32_t c, uint32_t d, bool u_loop) {
+  if (c == 0u && d < GW_BS_PACK_D && !u_loop) return kMetaStashOk;  // list mode, meta 0
   return bs_meta(c, d);
-}
-
-// first index in [b, e) with nbrs[i] >= key
-__device__ __forceinline__ int64_t lower_bound_i32(const int32_t* __restrict__ a, int64_t b, int64_t e, int32_t key) {
-  while (b < e) {
-    const int64_t mid = (b + e) >> 1;
-    if (a[mid] < key)
-      b = mid + 1;
-    else
-      e = mid;
-  }
-  return b;
-}
-
-struct BsSlot {
-  int32_t u;
-  int64_t ub, ue, vb, ve;
-};
-
-__device__ __forceinline__ BsSlot bs_slot(const gw_dev_graph& G, int64_t e) {
-  BsSlot S;
-  const int32_t v = G.nbrs[e];
-  S.u = row_of_slot(G.offsets, G.n, e);
-  S.ub = G.offsets[S.u];
-  S.ue = G.offsets[S.u + 1];
-  S.vb = G.offsets[v];
-  S.ve = G.offsets[v + 1];
-  return S;
-}
-
-// one thread: f(k, idx, kprev) per common position k (ascending), idx its rank
-template <class F>
-__device__ uint32_t common_thread(const gw_dev_graph& G, const BsSlot& S, F&& f) {
-  uint32_t c = 0;
-  int64_t kprev = -1;
-  if (S.ve - S.vb <= S.ue - S.ub) {
-    for (int64_t k = 0; k < S.ve - S.vb; ++k) {
-      const int32_t x = G.nbrs[S.vb + k];
-      if (x != S.u && bs_has_edge(G, S.ub, S.ue, x)) {
-        f(k, c++, kprev);
-        kprev = k;
-      }
-    }
-  } else {
-    int64_t lo = S.vb;
-    for (int64_t j = S.ub; j < S.ue && lo < S.ve; ++j) {
-      const int32_t x = G.nbrs[j];
-      if (x == S.u) continue;
-      lo = lower_bound_i32(G.nbrs, lo, S.ve, x);
-      if (lo < S.ve && G.nbrs[lo] == x) {
-        f(lo - S.vb, c++, kprev);
-        kprev = lo - S.vb;
-      }
-    }
-  }
-  return c;
-}
-
-// one wave: 64 probes per round; lanes holding a common position call f with
-// its rank and the previous common position (-1 for the first)
-template <class F>
-__device__ uint32_t common_wave(const gw_dev_graph& G, const BsSlot& S, F&& f, int64_t* klast) {
-  const int lane = threadIdx.x & 63;
-  const bool vside = S.ve - S.vb <= S.ue - S.ub;
-  const int64_t len = vside ? S.ve - S.vb : S.ue - S.ub;
-  uint32_t c = 0;
-  int carry = -1;
-  for (int64_t base = 0; base < len; base += 64) {
-    const int64_t j = base + lane;
-    bool found = false;
-    int k = 0;
-    if (j < len) {
-      if (vside) {
-        const int32_t x = G.nbrs[S.vb + j];
-        k = (int)j;
-        found = x != S.u && bs_has_edge(G, S.ub, S.ue, x);
-      } else {
-        const int32_t x = G.nbrs[S.ub + j];
-        if (x != S.u) {
-          const int64_t p = gw_row_find(G.nbrs, S.vb, S.ve, x);
-          if (p >= 0) {
-            found = true;
-            k = (int)(p - S.vb);
-          }
-        }
-      }
-    }
-    const unsigned long long m = __ballot(found);
-    if (!m) continue;
-    const unsigned long long lt = m & ((1ull << lane) - 1ull);
-    const int kp_in = __shfl(k, lt ? 63 - __clzll(lt) : 0, 64);
-    const int kl = __shfl(k, 63 - __clzll(m), 64);
-    if (found) f((int64_t)k, c + (uint32_t)__popcll(lt), (int64_t)(lt ? kp_in : carry));
-    c += (uint32_t)__popcll(m);
-    carry = kl;
-  }
-  *klast = carry;
-  return c;
 }
 
 // payload writer for one common position (entry words zeroed beforehand)
@@ -343,45 +242,6 @@ __device__ __forceinline__ BsEmit bs_emit(gw_bs_nbr* en, uint32_t* reg, const ui
   return E;
 }
 
-// pass 1 (slots with deg(v) > kSmallD): entry header {x, d, offsets[x], kp, c};
-// slots whose shorter row exceeds kThreadMin are queued for the wave kernel
-__global__ void k_bs_count(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn, int64_t* __restrict__ big,
-                           unsigned long long* __restrict__ nbig) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= G.nnz) return;
-  const int32_t v = G.nbrs[e];
-  const int64_t vb = G.offsets[v], d = G.offsets[v + 1] - vb;
-  if (d <= kSmallD) return;  // k_bs_fill_small
-  const BsSlot S = bs_slot(G, e);
-  const int64_t kp = gw_row_find(G.nbrs, S.vb, S.ve, S.u);
-  uint32_t c = 0;
-  if (min(S.ue - S.ub, d) <= kThreadMin)
-    c = common_thread(G, S, [](int64_t, uint32_t, int64_t) {});
-  else
-    big[atomicAdd(nbig, 1ull)] = e;
-  gw_bs_nbr* en = bsn + e;
-  *reinterpret_cast<uint4*>(en) = make_uint4((uint32_t)v, (uint32_t)d, (uint32_t)(uint64_t)vb, 0u);
-  const uint32_t k32 = kp >= 0 ? (uint32_t)(kp - vb) : 0xFFFFFFFFu;
-  *reinterpret_cast<uint2*>(&en->r[0]) =
-      d < GW_BS_PACK_D ? make_uint2((k32 & 0xFFFFu) | (c << 16), 0u) : make_uint2(k32, c);  // c: 0 if queued
-}
-
-__global__ void k_bs_count_wave(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn, const int64_t* __restrict__ big,
-                                const unsigned long long* __restrict__ nbig) {
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int64_t total = (int64_t)*nbig;
-  for (int64_t i = wave; i < total; i += nwaves) {
-    const int64_t e = big[i];
-    int64_t kl;
-    const uint32_t c = common_wave(G, bs_slot(G, e), [](int64_t, uint32_t, int64_t) {}, &kl);
-    if ((threadIdx.x & 63) == 0) {
-      if (bsn[e].d < GW_BS_PACK_D) bsn[e].r[0] |= c << 16;
-      else bsn[e].r[1] = c;
-    }
-  }
-}
-
 // region words per slot: only slots whose payload is neither list, inline nor Elias-Fano
 __global__ void k_bs_sizes(gw_dev_graph G, const gw_bs_nbr* __restrict__ bsn, uint64_t* __restrict__ sz,
                            int lists_only) {
@@ -392,105 +252,235 @@ __global__ void k_bs_sizes(gw_dev_graph G, const gw_bs_nbr* __restrict__ bsn, ui
               ? (uint64_t)bs_words(d) : 0ull;
 }
 
-// deg(v) <= kSmallD: one thread builds the whole entry (list or inline bitset)
-__global__ void k_bs_fill_small(gw_dev_graph G, gw_bs_nbr* __restrict__ bsn) {
-  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= G.nnz) return;
-  const int32_t v = G.nbrs[e];
-  const int64_t vb = G.offsets[v], d = G.offsets[v + 1] - vb;
-  if (d > kSmallD) return;
-  gw_bs_nbr en;
-  en.x = (uint32_t)v;
-  en.d = (uint32_t)d;
-  en.off = (uint32_t)vb;
-  en.meta = 0;
-#pragma unroll
-  for (int t = 0; t < 12; ++t) en.r[t] = 0;
-  const int32_t u = row_of_slot(G.offsets, G.n, e);
-  const int64_t ub = G.offsets[u], ue = G.offsets[u + 1];
-  uint32_t word = 0, c = 0, kp = 0xFFFFu;
-  for (int64_t k = 0; k < d; ++k) {
-    const int32_t x = G.nbrs[vb + k];
-    if (x == u) {
-      kp = (uint32_t)k;
-    } else if (bs_has_edge(G, ub, ue, x)) {
-      word |= 1u << (k & 31);
-      ++c;
-    }
-  }
-  en.r[0] = kp | (c << 16);  // d <= 32: packed header, payload r[1..11]
-  en.meta = bs_meta_slot(G, c, (uint32_t)d, u, ub, ue);
-  if (gw_bs_is_list(c, (uint32_t)d)) {  // sorted positions, 0xFFFF padded
-    uint16_t* lp = reinterpret_cast<uint16_t*>(en.r + 1);
-    for (int t = 0; t < 2 * 11; ++t) lp[t] = 0xFFFFu;
-    int t = 0;
-    for (uint32_t x = word; x; x &= x - 1) lp[t++] = (uint16_t)(__ffs(x) - 1);
-  } else {
-    en.r[1] = word;  // inline bitset (d <= 32)
-  }
-  bsn[e] = en;
+constexpr int kTB = 512;                     // build workgroup: 8 waves
+constexpr int kTW = kTB / 64;
+constexpr int kTriH = 4096;                  // ids of N(u) per hash chunk
+constexpr int kTriS = 2 * kTriH;             // LDS hash slots (load factor <= 1/2)
+constexpr int kTriEB = 512;                  // edges of u's row per work item
+
+// build-time model constants (gw_bitset_build_model_s), measured on MI355X
+constexpr double kBuildProbeRate = 5.0e11;     // k_bs_tri stream probes per second (one pass)
+constexpr double kBuildSlotSeconds = 2.0e-10;  // per adjacency slot: memset, headers, sizes scan, payload stores
+
+struct TriItem {
+  int32_t u, j0;  // vertex, first edge index in N(u) (items of a vertex: j0 = 0, kTriEB, ...)
+};
+
+// s_i = 1 iff vertex i has a self-loop (rows of NX_SIMPLE graphs are sorted)
+__global__ void k_bs_selfloop(gw_dev_graph G, uint8_t* __restrict__ loop) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= G.n) return;
+  loop[u] = gw_row_find(G.nbrs, G.offsets[u], G.offsets[u + 1], (int32_t)u) >= 0 ? 1 : 0;
 }
 
-// pass 2, one thread per slot (deg(v) > kSmallD, shorter row <= kThreadMin)
-__global__ void k_bs_fill_thread(gw_dev_graph G, const uint64_t* __restrict__ roff, uint32_t* __restrict__ reg,
-                                 gw_bs_nbr* __restrict__ bsn, int lists_only) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= G.nnz) return;
-  const int32_t v = G.nbrs[e];
-  const int64_t d = G.offsets[v + 1] - G.offsets[v];
-  if (d <= kSmallD) return;
-  const BsSlot S = bs_slot(G, e);
-  if (min(S.ue - S.ub, d) > kThreadMin) return;  // k_bs_fill_wave
-  gw_bs_nbr* en = bsn + e;
-  const uint32_t c = bs_c(en, (uint32_t)d);
-  uint32_t* w = bs_payload(en, (uint32_t)d);
-  en->meta = bs_meta_slot(G, c, (uint32_t)d, S.u, S.ub, S.ue);
-  if (lists_only && bs_mode(c, (uint32_t)d) == BS_REGION) {  // no payload: a draw filter, the walk probes
-    common_thread(G, S, [&](int64_t k, uint32_t, int64_t) { bs_filter_only(w, k, (uint32_t)d); });
-    return;
-  }
-  const BsEmit E = bs_emit(en, reg, roff, e, c, (uint32_t)d);
-  if (E.mode == BS_LIST) {
-    for (uint32_t t = c; t < 2 * gw_bs_pw((uint32_t)d); ++t) reinterpret_cast<uint16_t*>(w)[t] = 0xFFFFu;
-  } else if (E.mode == BS_REGION) {
-    w[0] = (uint32_t)(roff[e] / kBlk);  // regions are block aligned: 32-bit block index
-  }
-  int64_t klast = -1;
-  common_thread(G, S, [&](int64_t k, uint32_t idx, int64_t kprev) {
-    E(k, idx, kprev);
-    klast = k;
-  });
-  if (E.mode == BS_REGION) E.set_dir((klast < 0 ? -1 : klast / kDirBits) + 1, E.ndir - 1, c);
+__global__ void k_bs_iota(int64_t n, int32_t* __restrict__ a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) a[i] = (int32_t)i;
 }
 
-// pass 2, one wave per queued slot
-__global__ void k_bs_fill_wave(gw_dev_graph G, const uint64_t* __restrict__ roff, uint32_t* __restrict__ reg,
-                               gw_bs_nbr* __restrict__ bsn, const int64_t* __restrict__ big,
-                               const unsigned long long* __restrict__ nbig, int lists_only) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int64_t total = (int64_t)*nbig;
-  for (int64_t i = wave; i < total; i += nwaves) {
-    const int64_t e = big[i];
-    gw_bs_nbr* en = bsn + e;
-    const uint32_t d = en->d, c = bs_c(en, d);
-    uint32_t* w = bs_payload(en, d);
-    const BsSlot S = bs_slot(G, e);
-    if (lists_only && bs_mode(c, d) == BS_REGION) {  // no payload: a draw filter, the walk probes
-      if (lane == 0) en->meta = bs_meta(c, d);
-      int64_t kl;
-      common_wave(G, S, [&](int64_t k, uint32_t, int64_t) { bs_filter_only(w, k, d); }, &kl);
-      continue;
+// work items per vertex (in the degree-descending order): ceil(deg / kTriEB)
+__global__ void k_bs_nitems(gw_dev_graph G, const int32_t* __restrict__ order, uint32_t* __restrict__ nit) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > G.n) return;
+  nit[i] = i < G.n ? (uint32_t)((G.deg[order[i]] + kTriEB - 1) / kTriEB) : 0u;
+}
+
+__global__ void k_bs_items(gw_dev_graph G, const int32_t* __restrict__ order, const uint32_t* __restrict__ itoff,
+                           TriItem* __restrict__ items) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= G.n) return;
+  const int32_t u = order[i];
+  const uint32_t b = itoff[i], e = itoff[i + 1];
+  for (uint32_t t = b; t < e; ++t) items[t] = TriItem{u, (int32_t)((t - b) * kTriEB)};
+}
+
+// BsEmit for one slot of the edge (pass 2), or the lists-only draw filter
+struct TriSlot {
+  BsEmit E;
+  bool filt;  // lists-only build, region-size set: draw filter only
+  __device__ void operator()(int64_t k, uint32_t idx, int64_t kprev) const {
+    if (filt)
+      bs_filter_only(E.w, k, E.d);
+    else
+      E(k, idx, kprev);
+  }
+};
+
+__device__ __forceinline__ TriSlot tri_slot(gw_bs_nbr* en, uint32_t* reg, const uint64_t* roff, int64_t e, uint32_t c,
+                                            uint32_t d, int lists_only) {
+  TriSlot T;
+  T.filt = lists_only && bs_mode(c, d) == BS_REGION;
+  T.E = bs_emit(en, reg, roff, e, c, d);
+  return T;
+}
+
+// prologue of a slot's payload (pass 2): list padding, region block index
+__device__ __forceinline__ void tri_prologue(const TriSlot& T, int64_t e, uint32_t c, const uint64_t* roff, int lane) {
+  if (T.filt) return;
+  if (T.E.mode == BS_LIST && lane >= (int)c && lane < 2 * (int)gw_bs_pw(T.E.d))
+    reinterpret_cast<uint16_t*>(T.E.w)[lane] = 0xFFFFu;
+  if (T.E.mode == BS_REGION && lane == 0) T.E.w[0] = (uint32_t)(roff[e] / kBlk);
+}
+
+// epilogue (pass 2): directory blocks after the last common position
+__device__ __forceinline__ void tri_epilogue(const TriSlot& T, int64_t klast, uint32_t c, int lane) {
+  if (T.filt || T.E.mode != BS_REGION) return;
+  for (int64_t g = (klast < 0 ? -1 : klast / kDirBits) + 1 + lane; g < T.E.ndir; g += 64) T.E.set_dir(g, g, c);
+}
+
+__device__ __forceinline__ void tri_header(gw_bs_nbr* en, uint32_t x, uint32_t d, uint32_t off, uint32_t meta,
+                                           uint32_t kp, uint32_t c) {
+  *reinterpret_cast<uint4*>(en) = make_uint4(x, d, off, meta);
+  *reinterpret_cast<uint2*>(&en->r[0]) =
+      d < GW_BS_PACK_D ? make_uint2((kp & 0xFFFFu) | (c << 16), 0u) : make_uint2(kp, c);
+}
+
+// wave-level emission of this round's common positions of one slot: lanes
+// with `on` hold position pos; ranks continue from *cnt, kprev from *last
+template <class F>
+__device__ __forceinline__ void tri_emit(const F& f, bool on, int64_t pos, uint32_t* cnt, int64_t* last, int lane) {
+  const unsigned long long m = __ballot(on);
+  if (!m) return;
+  const unsigned long long lt = m & ((1ull << lane) - 1ull);
+  const int64_t pin = __shfl(pos, lt ? 63 - __clzll(lt) : 0, 64);
+  if (on) f(pos, *cnt + (uint32_t)__popcll(lt), lt ? pin : *last);
+  *last = __shfl(pos, 63 - __clzll(m), 64);
+  *cnt += (uint32_t)__popcll(m);
+}
+
+// (a launch's work-items must stay below 2^32, so a workgroup takes items
+// blockIdx.x, blockIdx.x + gridDim.x, ...; hubs come first in the item order)
+template <bool FILL>
+__global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* __restrict__ items, uint32_t nitems,
+                                                const uint8_t* __restrict__ loop, gw_bs_nbr* __restrict__ bsn,
+                                                const uint64_t* __restrict__ roff, uint32_t* __restrict__ reg,
+                                                int lists_only) {
+  __shared__ int32_t s_key[kTriS];
+  __shared__ uint16_t s_pos[kTriS];
+  // per-edge state between chunks (hubs): common counts, last positions, kp(u -> v), cursor in N(v)
+  __shared__ uint32_t s_cuv[kTriEB], s_cvu[kTriEB], s_cur[kTriEB];
+  __shared__ int32_t s_luv[kTriEB], s_lvu[kTriEB], s_kp[kTriEB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+    if (item != blockIdx.x) __syncthreads();  // every wave is done with the previous item's hash and state
+    const TriItem it = items[item];
+    const int32_t u = it.u;
+    const int64_t ub = G.offsets[u], du = G.offsets[u + 1] - ub;
+    const int64_t j0 = it.j0, j1 = min(du, j0 + (int64_t)kTriEB);
+    const int nch = (int)((du + kTriH - 1) / kTriH);
+    const int64_t hk = min(du, (int64_t)kTriH);  // keys per chunk (at most)
+    int lg = 6;
+    while ((1 << lg) < 2 * hk) ++lg;
+    const uint32_t S = 1u << lg, smask = S - 1u;
+    const int sh = 32 - lg;
+    const bool u_loop = loop[u] != 0;
+    for (int ch = 0; ch < nch; ++ch) {
+      const int64_t p0 = (int64_t)ch * kTriH, p1 = min(du, p0 + kTriH);
+      if (ch > 0) __syncthreads();  // every wave is done with the previous chunk
+      for (uint32_t i = tid; i < S; i += kTB) s_key[i] = -1;
+      __syncthreads();
+      for (int64_t i = tid; i < p1 - p0; i += kTB) {
+        const int32_t x = G.nbrs[ub + p0 + i];
+        uint32_t h = ((uint32_t)x * 0x9E3779B1u) >> sh;
+        while (atomicCAS(&s_key[h], -1, x) != -1) h = (h + 1) & smask;
+        s_pos[h] = (uint16_t)i;
+      }
+      __syncthreads();
+      // this chunk's id range is (previous chunk's last id, hi]: every element
+      // of N(v) falls in exactly one chunk's stream
+      const int32_t hi = ch == nch - 1 ? INT32_MAX : G.nbrs[ub + p1 - 1];
+      for (int64_t j = j0 + wave; j < j1; j += kTW) {
+        const int32_t v = G.nbrs[ub + j];
+        const int64_t vb = G.offsets[v], dv = G.offsets[v + 1] - vb;
+        if (!(du > dv || (du == dv && u <= v))) continue;  // the other end owns this edge
+        const int li = (int)(j - j0);
+        const int64_t e = ub + j;
+        uint32_t cuv = 0, cvu = 0, cur = 0;
+        int64_t luv = -1, lvu = -1, kp = -1;
+        if (ch > 0) {
+          cuv = s_cuv[li];
+          cvu = s_cvu[li];
+          cur = s_cur[li];
+          luv = s_luv[li];
+          lvu = s_lvu[li];
+          kp = s_kp[li];
+        }
+        // pass 2: both slots' payload writers (headers from pass 1)
+        TriSlot Tuv, Tvu;
+        int64_t er = -1;
+        if (FILL) {
+          gw_bs_nbr* en = bsn + e;
+          const uint32_t c = bs_c(en, (uint32_t)dv);
+          Tuv = tri_slot(en, reg, roff, e, c, (uint32_t)dv, lists_only);
+          if (ch == 0) tri_prologue(Tuv, e, c, roff, lane);
+          if (u != v) {
+            const uint32_t kpv = (uint32_t)dv < GW_BS_PACK_D ? (en->r[0] & 0xFFFFu) : en->r[0];
+            er = vb + kpv;  // the reverse slot (v -> u)
+            gw_bs_nbr* enr = bsn + er;
+            const uint32_t cr = bs_c(enr, (uint32_t)du);
+            Tvu = tri_slot(enr, reg, roff, er, cr, (uint32_t)du, lists_only);
+            if (ch == 0) tri_prologue(Tvu, er, cr, roff, lane);
+          }
+        }
+        for (;;) {
+          const int64_t k = (int64_t)cur + lane;
+          const int32_t x = k < dv ? G.nbrs[vb + k] : INT32_MAX;
+          const bool inr = k < dv && x <= hi;
+          bool hit = false;
+          uint32_t pu = 0;
+          if (inr) {
+            uint32_t h = ((uint32_t)x * 0x9E3779B1u) >> sh;
+            for (;;) {
+              const int32_t kk = s_key[h];
+              if (kk == x) {
+                hit = true;
+                pu = (uint32_t)p0 + s_pos[h];
+                break;
+              }
+              if (kk == -1) break;
+              h = (h + 1) & smask;
+            }
+          }
+          const unsigned long long mu = __ballot(inr && x == u);
+          if (mu) kp = (int64_t)cur + (__ffsll(mu) - 1);
+          const bool cu = hit && x != u;              // (u -> v): position k in N(v)
+          const bool cv = hit && x != v && u != v;    // (v -> u): position pu in N(u)
+          if (FILL) {
+            tri_emit(Tuv, cu, k, &cuv, &luv, lane);
+            if (u != v) tri_emit(Tvu, cv, (int64_t)pu, &cvu, &lvu, lane);
+          } else {
+            const unsigned long long m1 = __ballot(cu), m2 = __ballot(cv);
+            cuv += (uint32_t)__popcll(m1);
+            cvu += (uint32_t)__popcll(m2);
+          }
+          const int nin = __popcll(__ballot(inr));  // a prefix of the lanes (rows are sorted)
+          cur += (uint32_t)nin;
+          if (nin < 64) break;  // the chunk's id range or the row ended
+        }
+        if (ch + 1 < nch) {
+          if (lane == 0) {
+            s_cuv[li] = cuv;
+            s_cvu[li] = cvu;
+            s_cur[li] = cur;
+            s_luv[li] = (int32_t)luv;
+            s_lvu[li] = (int32_t)lvu;
+            s_kp[li] = (int32_t)kp;
+          }
+          continue;
+        }
+        if (FILL) {
+          tri_epilogue(Tuv, luv, cuv, lane);
+          if (u != v) tri_epilogue(Tvu, lvu, cvu, lane);
+        } else {
+          const uint32_t k32 = kp >= 0 ? (uint32_t)kp : 0xFFFFFFFFu;
+          if (lane == 0)
+            tri_header(bsn + e, (uint32_t)v, (uint32_t)dv, (uint32_t)vb, bs_meta_slot(cuv, (uint32_t)dv, u_loop), k32, cuv);
+          if (lane == 1 && u != v && kp >= 0)
+            tri_header(bsn + vb + kp, (uint32_t)u, (uint32_t)du, (uint32_t)ub,
+                       bs_meta_slot(cvu, (uint32_t)du, loop[v] != 0), (uint32_t)j, cvu);
+        }
+      }
     }
-    const BsEmit E = bs_emit(en, reg, roff, e, c, d);
-    if (E.mode == BS_LIST && lane >= (int)c && lane < 2 * (int)gw_bs_pw(d)) reinterpret_cast<uint16_t*>(w)[lane] = 0xFFFFu;
-    if (E.mode == BS_REGION && lane == 0) w[0] = (uint32_t)(roff[e] / kBlk);
-    if (lane == 0) en->meta = bs_meta_slot(G, c, d, S.u, S.ub, S.ue);
-    int64_t klast;
-    common_wave(G, S, E, &klast);
-    if (E.mode == BS_REGION)
-      for (int64_t g = (klast < 0 ? -1 : klast / kDirBits) + 1 + lane; g < E.ndir; g += 64) E.set_dir(g, g, c);
   }
 }
 
@@ -1230,16 +1220,35 @@ void gw_dev_bitset_release(gw_graph* g) {
   bs_free(g->d.bs_nbr);
 }
 
-// Build the per-edge entries and regions.  Uses the membership bitmap
-// (has_edge) when present.  Regions are sized from the exact common-neighbour
-// counts (pass 1), so slots whose payload fits the entry take no region space.
-// lists_only: no regions at all — entries whose payload would need one keep
-// mode BS_REGION and no payload (the rejection sampler's listed entries,
-// k_walk_listed, probes for those).
+// sum over undirected edges of min(deg u, deg v) = k_bs_tri's probes (each
+// edge counted at its owner u, where min = deg v)
+__global__ void k_bs_work(gw_dev_graph G, unsigned long long* __restrict__ acc) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long w = 0;
+  if (u < G.n) {
+    const int64_t ub = G.offsets[u], du = G.offsets[u + 1] - ub;
+    for (int64_t j = 0; j < du; ++j) {
+      const int32_t v = G.nbrs[ub + j];
+      const int64_t dv = G.deg[v];
+      if (du > dv || (du == dv && u <= v)) w += (unsigned long long)dv;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) w += __shfl_down(w, o, 64);
+  if ((threadIdx.x & 63) == 0 && w) atomicAdd(acc, w);
+}
+
+// Build the per-edge entries and regions (k_bs_tri, see the build section):
+// pass 1 writes every slot's header, regions are sized from the exact
+// (c, d) (slots whose payload fits the entry take no region space) and
+// placed by a scan, pass 2 writes the payloads.  Work items are scheduled
+// hubs first (vertices in degree-descending order).  lists_only: no regions
+// at all — entries whose payload would need one keep mode BS_REGION and a
+// draw filter (the rejection sampler's listed entries, k_walk_listed, probes
+// for those).
 int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
   gw_dev_graph& d = g->d;
   gw_dev_bitset_release(g);
-  const int64_t nnz = g->nnz;
+  const int64_t nnz = g->nnz, n = g->n;
   if (nnz == 0) return GW_OK;
   if (nnz >= (int64_t)0xFFFFFFFF) {  // the walk kernel passes slot indices as u32
     g->err = "bitset mode supports < 2^32 - 1 adjacency entries: use GW_N2V_REJECTION";
@@ -1253,69 +1262,122 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
   int rc;
   uint64_t* sz = nullptr;
   uint64_t* roff = nullptr;
-  int64_t* big = nullptr;
-  unsigned long long* nbig = nullptr;
+  uint8_t* loop = nullptr;
+  int32_t *ids = nullptr, *order = nullptr;
+  uint32_t* nit = nullptr;
+  uint32_t* itoff = nullptr;
+  TriItem* items = nullptr;
+  void* tmp = nullptr;
   auto cleanup = [&]() {
     bs_free(sz);
     bs_free(roff);
-    bs_free(big);
-    bs_free(nbig);
+    bs_free(loop);
+    bs_free(ids);
+    bs_free(order);
+    bs_free(nit);
+    bs_free(itoff);
+    bs_free(items);
+    bs_free(tmp);
   };
-  if ((rc = bs_alloc(g, &d.bs_nbr, nnz)) || (rc = bs_alloc(g, &big, nnz)) || (rc = bs_alloc(g, &nbig, 1)) ||
-      (rc = bs_alloc(g, &sz, nnz + 1)) || (rc = bs_alloc(g, &roff, nnz + 1))) {
+  auto fail = [&](int code) {
     cleanup();
     gw_dev_bitset_release(g);
-    return rc;
-  }
+    return code;
+  };
+#define BS_TRY(expr)                                                 \
+  do {                                                               \
+    hipError_t _e = (expr);                                          \
+    if (_e != hipSuccess) {                                          \
+      g->err = std::string(#expr) + ": " + hipGetErrorString(_e);    \
+      return fail(GW_ERR_DEVICE);                                    \
+    }                                                                \
+  } while (0)
+  if ((rc = bs_alloc(g, &d.bs_nbr, nnz)) || (rc = bs_alloc(g, &loop, n)) || (rc = bs_alloc(g, &ids, n)) ||
+      (rc = bs_alloc(g, &order, n)) || (rc = bs_alloc(g, &nit, n + 1)) || (rc = bs_alloc(g, &itoff, n + 1)))
+    return fail(rc);
+  const unsigned gn = (unsigned)((n + kB - 1) / kB), gn1 = (unsigned)((n + 1 + kB - 1) / kB);
+  BS_TRY(hipMemset(d.bs_nbr, 0, (size_t)nnz * sizeof(gw_bs_nbr)));
+  k_bs_selfloop<<<gn, kB>>>(d, loop);
+  k_bs_iota<<<gn, kB>>>(n, ids);
+  BS_TRY(hipGetLastError());
+  // work items: vertices by degree, descending (hubs first), kTriEB edges each
+  size_t tb = 0, tb2 = 0;
+  BS_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                                      (const int32_t*)nullptr, (int32_t*)nullptr, (int)n));
+  BS_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, nit, itoff, (int)(n + 1)));
+  if ((rc = bs_alloc(g, (char**)&tmp, (int64_t)std::max(tb, tb2) + 1))) return fail(rc);
+  int32_t* dkey = nullptr;  // sorted degrees (discarded)
+  if ((rc = bs_alloc(g, &dkey, n))) return fail(rc);
+  BS_TRY(hipcub::DeviceRadixSort::SortPairsDescending(tmp, tb, d.deg, dkey, ids, order, (int)n));
+  bs_free(dkey);
+  k_bs_nitems<<<gn1, kB>>>(d, order, nit);
+  BS_TRY(hipGetLastError());
+  BS_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, nit, itoff, (int)(n + 1)));
+  uint32_t nitems = 0;
+  BS_TRY(hipMemcpy(&nitems, itoff + n, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if ((rc = bs_alloc(g, &items, std::max<int64_t>(nitems, 1)))) return fail(rc);
+  k_bs_items<<<gn, kB>>>(d, order, itoff, items);
+  BS_TRY(hipGetLastError());
+  bs_free(tmp);
+  bs_free(ids);
+  bs_free(order);
+  bs_free(nit);
+  bs_free(itoff);
+  // pass 1: headers
+  const unsigned tgrid = std::min<uint32_t>(nitems, 1u << 20);  // <= 2^29 work-items per launch
+  if (nitems) k_bs_tri<false><<<tgrid, kTB>>>(d, items, nitems, loop, d.bs_nbr, nullptr, nullptr, lists_only ? 1 : 0);
+  BS_TRY(hipGetLastError());
+  // region layout
+  if ((rc = bs_alloc(g, &sz, nnz + 1)) || (rc = bs_alloc(g, &roff, nnz + 1))) return fail(rc);
   const unsigned grid = (unsigned)((nnz + kB - 1) / kB);
-  GW_HIP_TRY(hipMemset(d.bs_nbr, 0, (size_t)nnz * sizeof(gw_bs_nbr)));
-  GW_HIP_TRY(hipMemset(nbig, 0, sizeof(unsigned long long)));
-  k_bs_count<<<grid, kB>>>(d, d.bs_nbr, big, nbig);
-  GW_HIP_TRY(hipGetLastError());
-  k_bs_count_wave<<<4096, kB>>>(d, d.bs_nbr, big, nbig);
-  GW_HIP_TRY(hipGetLastError());
   k_bs_sizes<<<grid, kB>>>(d, d.bs_nbr, sz, lists_only ? 1 : 0);
-  GW_HIP_TRY(hipGetLastError());
-  GW_HIP_TRY(hipMemset(sz + nnz, 0, sizeof(uint64_t)));
+  BS_TRY(hipGetLastError());
+  BS_TRY(hipMemset(sz + nnz, 0, sizeof(uint64_t)));
   size_t tmpb = 0;
-  GW_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmpb, sz, roff, nnz + 1));
-  void* tmp = nullptr;
-  if ((rc = bs_alloc(g, (char**)&tmp, (int64_t)tmpb + 1))) {
-    cleanup();
-    gw_dev_bitset_release(g);
-    return rc;
-  }
-  GW_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmpb, sz, roff, nnz + 1));
-  GW_HIP_TRY(hipDeviceSynchronize());
+  BS_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmpb, sz, roff, nnz + 1));
+  if ((rc = bs_alloc(g, (char**)&tmp, (int64_t)tmpb + 1))) return fail(rc);
+  BS_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmpb, sz, roff, nnz + 1));
+  BS_TRY(hipDeviceSynchronize());
   bs_free(tmp);
   bs_free(sz);
   uint64_t words = 0;
-  GW_HIP_TRY(hipMemcpy(&words, roff + nnz, sizeof(uint64_t), hipMemcpyDeviceToHost));
+  BS_TRY(hipMemcpy(&words, roff + nnz, sizeof(uint64_t), hipMemcpyDeviceToHost));
   const int64_t need = (int64_t)words * 4 + nnz * (int64_t)sizeof(gw_bs_nbr);
   if (need > budget_bytes) {
-    cleanup();
-    gw_dev_bitset_release(g);
     g->err = "per-edge bitsets need " + std::to_string(need) + " B; over the " + std::to_string(budget_bytes) +
              " B budget: use GW_N2V_REJECTION";
-    return GW_ERR_CAPACITY;
+    return fail(GW_ERR_CAPACITY);
   }
   if (words == 0) words = 1;  // no region at all: keep a valid pointer
-  if ((rc = bs_alloc(g, &d.bs_region, (int64_t)words))) {
-    cleanup();
-    gw_dev_bitset_release(g);
-    return rc;
-  }
-  GW_HIP_TRY(hipMemset(d.bs_region, 0, (size_t)words * 4));
-  k_bs_fill_small<<<grid, kB>>>(d, d.bs_nbr);
-  GW_HIP_TRY(hipGetLastError());
-  k_bs_fill_thread<<<grid, kB>>>(d, roff, d.bs_region, d.bs_nbr, lists_only ? 1 : 0);
-  GW_HIP_TRY(hipGetLastError());
-  k_bs_fill_wave<<<4096, kB>>>(d, roff, d.bs_region, d.bs_nbr, big, nbig, lists_only ? 1 : 0);
-  GW_HIP_TRY(hipGetLastError());
-  GW_HIP_TRY(hipDeviceSynchronize());
+  if ((rc = bs_alloc(g, &d.bs_region, (int64_t)words))) return fail(rc);
+  BS_TRY(hipMemset(d.bs_region, 0, (size_t)words * 4));
+  // pass 2: payloads
+  if (nitems)
+    k_bs_tri<true><<<tgrid, kTB>>>(d, items, nitems, loop, d.bs_nbr, roff, d.bs_region, lists_only ? 1 : 0);
+  BS_TRY(hipGetLastError());
+  BS_TRY(hipDeviceSynchronize());
+#undef BS_TRY
   cleanup();
   g->bitset_words = (int64_t)words;
   return GW_OK;
+}
+
+// Modelled wall time of gw_dev_bitset_build on this graph: two k_bs_tri
+// passes over sum(min(deg u, deg v)) probes plus per-slot header / payload
+// traffic, at rates measured on MI355X; < 0 on a device error.
+double gw_bitset_build_model_s(gw_graph* g) {
+  unsigned long long* acc = nullptr;
+  if (hipMalloc((void**)&acc, sizeof(unsigned long long)) != hipSuccess) return -1.0;
+  unsigned long long w = 0;
+  bool ok = hipMemset(acc, 0, sizeof w) == hipSuccess;
+  if (ok && g->n > 0) {
+    k_bs_work<<<(unsigned)((g->n + kB - 1) / kB), kB>>>(g->d, acc);
+    ok = hipGetLastError() == hipSuccess;
+  }
+  ok = ok && hipMemcpy(&w, acc, sizeof w, hipMemcpyDeviceToHost) == hipSuccess;
+  (void)hipFree(acc);
+  if (!ok) return -1.0;
+  return 2.0 * (double)w / kBuildProbeRate + (double)g->nnz * kBuildSlotSeconds;
 }
 
 int gw_dev_walk_bitset_launch(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int64_t walk_count,

@@ -353,10 +353,10 @@ int gw_dev_simrank_naive(gw_graph* g, double C, int iters, double* sim_dev, void
     GW_HIP_TRY(hipGetLastError());
     SrArgs A{m, g->sr_off, g->sr_ent, g->sr_heads, C};
     // input row in LDS when it leaves room for a window of SR_MIN_WIN rows;
-    // GW_SIMRANK_HBM_ROW=1 selects the HBM-row variant (same bits; tests compare the two)
-    const char* diag = std::getenv("GW_SIMRANK_HBM_ROW");
+    // the handle's simrank_hbm_row option selects the HBM-row variant (same
+    // bits; tests compare the two)
     const int64_t cap = SR_LDS_BYTES / (int64_t)sizeof(double);
-    const bool lds_row = m + SR_MIN_WIN <= cap && !(diag && diag[0] == '1');
+    const bool lds_row = m + SR_MIN_WIN <= cap && !g->opt.simrank_hbm_row;
     const int win = (int)std::min<int64_t>(m, lds_row ? cap - m : cap);
     for (int r = 0; r < iters; ++r) {  // while (r++ < STEP), SimRank.java:38
       const int last = r == iters - 1;

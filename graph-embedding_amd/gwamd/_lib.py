@@ -75,6 +75,13 @@ class GraphInfo(ctypes.Structure):
                 ("sampler_bytes", ctypes.c_int64)]
 
 
+class Options(ctypes.Structure):
+    """gw_options_t (per-handle tuning, include/graphwalk.h)."""
+    _fields_ = [("table_budget_bytes", ctypes.c_int64), ("expected_steps", ctypes.c_int64),
+                ("listed", ctypes.c_int32), ("simrank_hbm_row", ctypes.c_int32),
+                ("host_chunk_bytes", ctypes.c_int64)]
+
+
 P = ctypes.c_void_p
 I32 = ctypes.c_int32
 I64 = ctypes.c_int64
@@ -98,6 +105,8 @@ SIGNATURES = {
     "gw_graph_rmat": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, D, D, D, U64, PP]),
     "gw_graph_rmat_java": (ctypes.c_int, [I64, I64, D, D, D, U64, PP]),
     "gw_graph_info": (ctypes.c_int, [P, ctypes.POINTER(GraphInfo)]),
+    "gw_graph_set_options": (ctypes.c_int, [P, ctypes.POINTER(Options)]),
+    "gw_graph_get_options": (ctypes.c_int, [P, ctypes.POINTER(Options)]),
     "gw_graph_export_csr": (ctypes.c_int, [P, P, P, P, P, P]),
     "gw_graph_free": (ctypes.c_int, [P]),
     "gw_graph_to_device": (ctypes.c_int, [P, ctypes.c_int]),

@@ -99,6 +99,9 @@ def _scale(args):
             dist.init_process_group(args.dist_backend)
     g = GWGraph.from_edgelist(args.input, args.delimiter, "nx", args.directed, args.weighted)
     g.to_device(device)
+    # the walks this rank will run on this preparation: the sampler's optional
+    # tables are built only when they pay back within them (gw_options_t)
+    g.options(expected_steps=gd.shard_range(args.num_walks * g.n, world, rank)[1] * (args.walk_length - 1))
     mode = C.N2V_REJECTION
     if args.sampler != "rejection" and not args.directed and not args.weighted and (args.p, args.q) != (1.0, 1.0):
         try:

@@ -107,6 +107,20 @@ class GWGraph:
         C.check(C.lib().gw_graph_info(self._h, ctypes.byref(inf)), self._h)
         return inf
 
+    def options(self, **kw):
+        """Read, and with keyword arguments update, the handle's gw_options_t
+        (table_budget_bytes, expected_steps, listed, simrank_hbm_row,
+        host_chunk_bytes).  Returns the options in effect as a dict."""
+        o = C.Options()
+        C.check(C.lib().gw_graph_get_options(self._h, ctypes.byref(o)), self._h)
+        for k, v in kw.items():
+            if not hasattr(o, k):
+                raise TypeError(f"unknown option {k!r}")
+            setattr(o, k, int(v))
+        if kw:
+            C.check(C.lib().gw_graph_set_options(self._h, ctypes.byref(o)), self._h)
+        return {f: getattr(o, f) for f, _ in C.Options._fields_}
+
     @property
     def n(self):
         return self.info().n

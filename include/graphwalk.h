@@ -104,6 +104,28 @@ typedef struct gw_graph_info_t {
                             (bitset entries + regions, or rejection slot entries) */
 } gw_graph_info_t;
 
+/* Per-handle tuning (gw_graph_set_options).  Sizes and sampler choices
+ * only: the walks and scores a call returns do not depend on any of them
+ * (tested).  These replace what earlier versions read from environment
+ * variables, so the library reads no process-global state.               */
+typedef struct gw_options_t {
+  /* cap on the node2vec sampler's per-slot tables (bitset entries + regions,
+   * listed entries, 16 B slot entries); 0 = half of the free HBM at prepare */
+  int64_t table_budget_bytes;
+  /* walk steps the caller intends to run on one gw_n2v_prepare; with
+   * listed = -1, GW_N2V_REJECTION builds its 64 B listed entries only when
+   * their modelled build time is paid back over these steps; 0 = unknown   */
+  int64_t expected_steps;
+  /* GW_N2V_REJECTION listed entries: -1 = by expected_steps (unknown: build
+   * whenever they fit), 0 = never, 1 = whenever they fit                   */
+  int32_t listed;
+  /* gw_simrank_naive input row: 0 = in LDS when it fits, 1 = in HBM (same
+   * result bits; exists for tests and very large m)                        */
+  int32_t simrank_hbm_row;
+  /* gw_n2v_walks_host staging chunk in bytes; 0 = 256 MB                   */
+  int64_t host_chunk_bytes;
+} gw_options_t;
+
 typedef struct gw_topsim_stats_t {
   int64_t extensions;   /* path extensions (queue.add, TopSim_singleSample.java:115,147) */
   int64_t pair_updates; /* executions of TopSim_singleSample.java:189                     */
@@ -161,6 +183,11 @@ int gw_graph_info(const gw_graph* g, gw_graph_info_t* info);
 int gw_graph_export_csr(const gw_graph* g, int64_t* offsets, int32_t* nbrs,
                         double* weights, int64_t* labels, int32_t* node_order);
 int gw_graph_free(gw_graph* g);
+
+/* Options of this handle (defaults: all zero, listed = -1); opt NULL resets
+ * the defaults.  Take effect at the next call that uses them.               */
+int gw_graph_set_options(gw_graph* g, const gw_options_t* opt);
+int gw_graph_get_options(const gw_graph* g, gw_options_t* opt);
 
 /* Upload CSR (+degree, weight sums) to HBM of `device`.                     */
 int gw_graph_to_device(gw_graph* g, int device);

@@ -49,6 +49,43 @@ def test_bench_multi_rank_plumbing(ranks, limit):
         assert g["mode"] == "whole"
 
 
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_bench_config4_strong_plumbing(ranks):
+    """Config 4's BASELINE shape (the r=10 workload split over
+    the GPUs, walks all-gathered): shard_range shards (uneven by one walk,
+    padded for the collective), the summed walk-steps equal ONE pass of the
+    fixed workload per step whatever the rank count, and the gathered block
+    of the last rank equals rank 0's recomputation of it."""
+    steps, scale, L, r = 2, 8, 80, 10
+    rc, res, err = _run(["--gpus", str(ranks), "--plumbing-check", "--config", "4", "--scale", str(scale),
+                         "--steps", str(steps), "--warmup", "1"])
+    assert rc == 0, err[-2000:]
+    total = r * (1 << scale)
+    assert res["scaling"] == "strong" and res["ranks"] == ranks
+    assert res["config"]["walks_per_step"] == total and "strong" in res["config"]["parallelism"]
+    assert res["walk_steps"] == steps * total * (L - 1)
+    g = res["allgather"]
+    assert g["check_last_rank_block_identical"] is True and res["allgather_all_ranks_ok"] is True
+    rows = -(-total // ranks)
+    assert g["gathered_bytes_per_step_per_rank"] == (ranks - 1) * rows * L * 4
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_bench_config5_rows_allgather_plumbing(ranks):
+    """Config 5's exchange (k x (int32 + fp64) per source): the
+    round-robin source shards' top-100 rows all-gathered to every rank, each
+    received block checked against its sender's checksum."""
+    scale, K = 8, 100
+    rc, res, err = _run(["--gpus", str(ranks), "--plumbing-check", "--config", "5", "--scale", str(scale),
+                         "--steps", "2"])
+    assert rc == 0, err[-2000:]
+    assert res["scaling"] == "strong" and res["ranks"] == ranks
+    g = res["allgather"]
+    assert g["check_blocks_match_sender_checksums"] is True
+    rows = -(-(1 << scale) // ranks)
+    assert g["gathered_bytes_per_step_per_rank"] == (ranks - 1) * rows * K * 12
+
+
 def test_bench_rank_count_mismatch_is_refused():
     rc, res, err = _run(["--gpus", "2", "--plumbing-check"], {"WORLD_SIZE": "1"}, timeout=120)
     assert rc == 2 and res is None

@@ -352,6 +352,41 @@ def test_release_library_has_no_diagnostic_knobs(gw):
     assert b"GW_DIAG" not in blob
 
 
+def test_release_library_reads_no_environment_knobs(gw):
+    """Sizing / sampler choices are per-handle options (gw_graph_set_options),
+    not environment variables: no source of the library calls getenv except
+    through the -DGW_DIAG-only GW_DIAG_ENV macro, and the release binary names
+    none of the former knobs.  (The only getenv left in the binary is rocPRIM's
+    own ROCPRIM_USE_ATOMIC_BLOCK_ID, inside its device scan.)"""
+    import glob
+    from gwamd import _lib
+    srcs = glob.glob(os.path.join(ROOT, "graph-embedding_amd", "csrc", "*"))
+    for f in srcs:
+        txt = open(f).read()
+        for m in re.finditer(r"\bgetenv\s*\(", txt):
+            line = txt[:m.start()].count("\n") + 1
+            assert f.endswith("gw_internal.h") and "GW_DIAG_ENV" in txt.splitlines()[line - 1], (f, line)
+    if os.path.basename(_lib.LIB_PATH) != "libgraphwalk.so":
+        pytest.skip("GW_LIB points at a non-release library")
+    blob = open(_lib.LIB_PATH, "rb").read()
+    for knob in (b"GW_SENT_MAX_GB", b"GW_BITSET_BUDGET_GB", b"GW_HOST_CHUNK_MB", b"GW_SIMRANK_HBM_ROW"):
+        assert knob not in blob
+
+
+def test_options_roundtrip_and_validation(gw):
+    import ctypes
+    from gwamd import _lib as C
+    G = gw.GWGraph.from_edgelist(os.path.join(DATA, "karate.edgelist"), " ", "nx")
+    d = G.options()
+    assert d == dict(table_budget_bytes=0, expected_steps=0, listed=-1, simrank_hbm_row=0, host_chunk_bytes=0)
+    d = G.options(expected_steps=123, listed=0, host_chunk_bytes=1 << 20)
+    assert d["expected_steps"] == 123 and d["listed"] == 0 and d["host_chunk_bytes"] == 1 << 20
+    bad = C.Options(0, 0, 2, 0, 0)
+    assert C.lib().gw_graph_set_options(G.handle, ctypes.byref(bad)) == C.GW_ERR_INVALID
+    assert C.lib().gw_graph_set_options(G.handle, None) == 0
+    assert G.options()["listed"] == -1
+
+
 def test_java_double_to_string_matches_java(gw, oracle):
     """gw_format_java_double == Java's Double.toString (Eval.java:118 writes
     precision values this way) on known Java outputs and random doubles."""

@@ -541,7 +541,7 @@ def test_walks_host_pipeline_equals_device(gw, mode, monkeypatch):
     C.check(C.lib().gw_n2v_walks(G.handle, L, 9, begin, count, 1, C.ptr(out), C.ptr(lens), C.ptr(cnt), None),
             G.handle)
     torch.cuda.synchronize()
-    monkeypatch.setenv("GW_HOST_CHUNK_MB", "1")  # 6,553 walks per chunk: 5 chunks
+    G.options(host_chunk_bytes=1 << 20)  # 6,553 walks per chunk: 5 chunks
     W = np.empty((count, L), np.int32)
     ln = np.empty(count, np.int32)
     hc = np.zeros(2, np.uint64)

@@ -58,12 +58,12 @@ def test_naive_simrank_reference_fixture(gw):
                 assert abs(sim[v, int(i)] - float(val)) <= 5.1e-9
 
 
-def test_naive_simrank_global_row_path_bitwise(gw, monkeypatch):
+def test_naive_simrank_global_row_path_bitwise(gw):
     """The HBM-row variant (n*8 > LDS budget) gives the same bits as the
     LDS-row variant (same reduction order)."""
     g = _graph("moreno")
     a = _gpu(g, 0.6, 3)
-    monkeypatch.setenv("GW_SIMRANK_HBM_ROW", "1")
+    g._g.options(simrank_hbm_row=1)
     b = _gpu(g, 0.6, 3)
     assert np.array_equal(a, b)
 
