@@ -110,6 +110,8 @@ def parse(argv):
     ap.add_argument("--topsim-sample", type=int, default=10000)
     ap.add_argument("--topsim-step", type=int, default=5)
     ap.add_argument("--topsim-graphs", default="blog", help="comma list of blog,arxiv,moreno")
+    ap.add_argument("--p10m-vertices", type=int, default=10_000_000,
+                    help="config 5 graph size (BASELINE: 10M vertices, 10 R-MAT lines per vertex); smaller for tests")
     ap.add_argument("--plumbing-check", action="store_true",
                     help="ranks + collectives with synthetic rows, no GPU work, no throughput")
     a = ap.parse_args(argv)
@@ -647,6 +649,27 @@ def walk_headline(R, args):
         res["cpu_baseline"] = cpu_baseline_walks(G.export_csr(), args.p, args.q, args.seed, L, 0, args.cpu_seconds)
     if rank == 0:
         res["copy_gbps"] = stream_copy_gbps(R)
+    if mode == "bitset" and world == 1:
+        # the same BASELINE pass end to end with the plain rejection sampler
+        # (16 B slot entries + neighbour hash, no per-edge tables): the
+        # sampler a one-shot run should pick is the faster end to end
+        G.options(listed=0)
+        t0 = time.perf_counter()
+        C.check(C.lib().gw_n2v_prepare(G.handle, args.p, args.q, C.N2V_REJECTION), G.handle)
+        torch.cuda.synchronize()
+        rprep = time.perf_counter() - t0
+        launch(first(0), cnt_w, out, None)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        launch(first(0), cnt_w, out, cnt)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        rw = e0.elapsed_time(e1) * 1e-3
+        alt = end_to_end(rprep, rw, launch_steps, 1.0, "prepare + one step, plain rejection sampler")
+        alt["walk_steps_per_s"] = launch_steps / rw
+        res["end_to_end_rejection"] = alt
+        res["end_to_end_best"] = "bitset" if res["end_to_end"]["total_s"] <= alt["total_s"] else "rejection"
     del out
     G.free()
     return res
@@ -855,7 +878,7 @@ def run_topsim(R, args, name):
         # 1e8 generated lines, all non-isolated sources, top-100
         t0 = time.perf_counter()
         a, b, c = rmat_abc(args)
-        pg = gwamd.GWGraph.rmat_java(10_000_000, 100_000_000, a, b, c, args.seed)
+        pg = gwamd.GWGraph.rmat_java(args.p10m_vertices, 10 * args.p10m_vertices, a, b, c, args.seed)
         csr = pg.export_csr()
         offs, nbrs = csr["offsets"], csr["nbrs"]
         deg = np.diff(offs)
@@ -867,8 +890,8 @@ def run_topsim(R, args, name):
         # ids, so contiguous ranges would load rank 0 with most of the work;
         # rows are keyed by source, so any split gives the same rows
         srcs = srcs_all[rank::world]
-        desc = (f"10M vertices, 1e8 R-MAT lines, {len(srcs_all)} non-isolated sources split round-robin over "
-                f"{world} rank(s)")
+        desc = (f"{args.p10m_vertices} vertices, {10 * args.p10m_vertices} R-MAT lines, {len(srcs_all)} non-isolated "
+                f"sources split round-robin over {world} rank(s)")
         K, sample, step = 100, 1000, 3
         scaling = "strong"
         keep = pg
@@ -905,6 +928,7 @@ def run_topsim(R, args, name):
             ev[1].record(stream)
     tel, kms = time_steps(R, tstep, 1, 0)
     ext_l, upd_l = int(st[0].item()), int(st[1].item())
+    ext, upd = (int(x) for x in R.allreduce([ext_l, upd_l], "sum", torch.int64))
     gather = None
     if name == "p10m" and world > 1 and args.allgather != "off":
         # every rank receives all top-k rows (k x (int32 + fp64)
@@ -927,7 +951,6 @@ def run_topsim(R, args, name):
                       value=upd / gboth["seconds"], unit="pair-updates/s (top-k rows all-gathered to every rank)",
                       check_blocks_match_sender_checksums=gonly["check_blocks_match_sender_checksums"] and
                       gboth["check_blocks_match_sender_checksums"])
-    ext, upd = (int(x) for x in R.allreduce([ext_l, upd_l], "sum", torch.int64))
     tag = f"topsim_{name}_s{sample}_t{step}_k{K}"
     cpu_ts = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -1148,10 +1171,11 @@ def main(argv):
                 "parallelism": f"replicated graph, walks sharded over {R.world} rank(s)" +
                                (" (the fixed r-walk workload split: strong scaling)" if args.config == 4 else "")}
             res["walk_steps"] = head["walk_steps"]
-            for k in ("mode", "prep_s", "sampler_gb", "trials_per_step", "end_to_end"):
+            for k in ("mode", "prep_s", "sampler_gb", "trials_per_step", "end_to_end", "end_to_end_rejection",
+                      "end_to_end_best"):
                 if k in head:
                     res[{"mode": "sampler", "prep_s": "prepare_seconds", "sampler_gb": "sampler_tables_gb",
-                         "trials_per_step": "rejection_trials_per_step", "end_to_end": "end_to_end"}[k]] = head[k]
+                         "trials_per_step": "rejection_trials_per_step"}.get(k, k)] = head[k]
             res["roofline"] = head.get("roofline")
             res["cpu_baseline"] = cpu
             if res["roofline"] is not None and R.rank == 0:

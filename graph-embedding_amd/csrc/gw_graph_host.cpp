@@ -639,6 +639,9 @@ struct JavaPQ {
 // round-trip digits; plain notation with at least one fraction digit for
 // 1e-3 <= |v| < 1e7, else computerized scientific "d.dddE[-]n" (JLS
 // Double.toString).  Eval.precision writes its scores this way (Eval.java:118).
+// Assumes JDK 19+ (JDK-4511638 fixed): JDK 8-18 print a few values with more
+// digits than the shortest repr; the reference commits no Eval output that
+// would pin the JDK it ran on.
 void gw_java_double_to_string(double v, std::string* out) {
   if (std::isnan(v)) {
     *out += "NaN";

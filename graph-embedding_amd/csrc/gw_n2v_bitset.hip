@@ -136,13 +136,19 @@ __device__ __forceinline__ int bs_mode(uint32_t c, uint32_t d) {
   return gw_bs_is_list(c, d) ? BS_LIST : gw_bs_is_inline(d) ? BS_INLINE : gw_bs_is_ef(c, d) ? BS_EF : BS_REGION;
 }
 
-// Return elision (k_walk_bitset): an entry E(u -> x) with c = 0 lets the walk
-// keep E(x -> u) in its empty payload words — valid only when c(x -> u) = 0
-// too.  The two common sets differ only by the origin (x's self-loop counts
-// in c(u -> x), u's in c(x -> u)), so the builder marks a c = 0 list entry
-// whose u has no self-loop with meta == kMetaStashOk; after the walk has
-// written its stash, meta == kMetaStash.
-constexpr uint32_t kMetaStashOk = 0x40000000u;
+// Return elision (k_walk_bitset).  When both directed slots of an edge have
+// small common sets (c(u -> x) <= kDualC and c(x -> u) <= kDualC, both
+// degrees < 65536), the builder writes E(u -> x) as a DUAL list entry: its
+// own positions in N(x) in payload halfwords 0..5, the positions in N(u) of
+// the reverse slot's common set (the payload of E(x -> u)) in halfwords 6..11,
+// meta = kMetaDual | c(x -> u) << 2 (mode LIST).  Arriving through it, the
+// walker keeps u's row and the index it drew at u in payload words 6..9
+// (kMetaStash), so E(x -> u) is fully known: a return move (draw == kp) swaps
+// rows, lists and counts in registers instead of fetching the reverse entry,
+// and a return after that swaps back.  Membership in a dual entry's list
+// looks at its first 3 words only.
+constexpr uint32_t kDualC = 6;
+constexpr uint32_t kMetaDual = 0x40000000u;
 constexpr uint32_t kMetaStash = 0x80000000u;
 
 // per-entry constants of the step kernel (no divisions per step):
@@ -157,16 +163,20 @@ __device__ __forceinline__ uint32_t bs_meta(uint32_t c, uint32_t d) {
   const uint32_t bblk = (mode == BS_REGION) ? (uint32_t)(bs_boff(d) / kBlk) : 0u;
   return mode | (l << 2) | (U << 7) | (bblk << 16);
 }
-// meta of slot (u -> x) with c common neighbours; u_loop: u has a self-loop
-__device__ __forceinline__ uint32_t bs_meta_slot(uint32_t c, uint32_t d, bool u_loop) {
-  if (c == 0u && d < GW_BS_PACK_D && !u_loop) return kMetaStashOk;  // list mode, meta 0
-  return bs_meta(c, d);
+// meta of slot (u -> x): c common neighbours, d = deg x; dual entries (see
+// above) carry the reverse slot's count c_rev (du = deg u)
+__device__ __forceinline__ bool bs_dual(uint32_t c, uint32_t c_rev, uint32_t d, uint32_t du) {
+  return c <= kDualC && c_rev <= kDualC && d < GW_BS_PACK_D && du < GW_BS_PACK_D;
+}
+__device__ __forceinline__ uint32_t bs_meta_slot(uint32_t c, uint32_t c_rev, uint32_t d, uint32_t du) {
+  return bs_dual(c, c_rev, d, du) ? (kMetaDual | (c_rev << 2)) : bs_meta(c, d);
 }
 
 // payload writer for one common position (entry words zeroed beforehand)
 struct BsEmit {
   int mode;
-  uint32_t* w;     // entry payload
+  bool nobits;     // region bits written by the caller (k_bs_tri's (u -> v) slot: whole words per round)
+  uint32_t* w;     // entry payload (or a staging copy of it)
   uint32_t* dir;   // region directory (ndir > kPDir)
   uint16_t* pdir;  // directory in the entry (0 < ndir <= kPDir)
   uint32_t* bits;  // region bits
@@ -189,7 +199,7 @@ struct BsEmit {
         if (sh + (uint32_t)l > 32u) atomicOr(&w[(off >> 5) + 1], lowv >> (32 - sh));
       }
     } else {
-      atomicOr(&bits[k >> 5], bit);
+      if (!nobits) atomicOr(&bits[k >> 5], bit);
       set_dir((kprev < 0 ? -1 : kprev / kDirBits) + 1, k / kDirBits, idx);
       // filter over the draw's high word y (bucket floor(y*F / 2^32)): the 64-bit draws
       // (y:z) with index k have y in [floor(k*2^32/d), ceil((k+1)*2^32/d) - 1]
@@ -220,6 +230,7 @@ __device__ __forceinline__ BsEmit bs_emit(gw_bs_nbr* en, uint32_t* reg, const ui
                                           uint32_t d) {
   BsEmit E;
   E.mode = bs_mode(c, d);
+  E.nobits = false;
   E.w = bs_payload(en, d);
   E.ndir = 0;
   E.dir = E.bits = nullptr;
@@ -266,13 +277,6 @@ struct TriItem {
   int32_t u, j0;  // vertex, first edge index in N(u) (items of a vertex: j0 = 0, kTriEB, ...)
 };
 
-// s_i = 1 iff vertex i has a self-loop (rows of NX_SIMPLE graphs are sorted)
-__global__ void k_bs_selfloop(gw_dev_graph G, uint8_t* __restrict__ loop) {
-  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= G.n) return;
-  loop[u] = gw_row_find(G.nbrs, G.offsets[u], G.offsets[u + 1], (int32_t)u) >= 0 ? 1 : 0;
-}
-
 __global__ void k_bs_iota(int64_t n, int32_t* __restrict__ a) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) a[i] = (int32_t)i;
@@ -294,10 +298,15 @@ __global__ void k_bs_items(gw_dev_graph G, const int32_t* __restrict__ order, co
   for (uint32_t t = b; t < e; ++t) items[t] = TriItem{u, (int32_t)((t - b) * kTriEB)};
 }
 
-// BsEmit for one slot of the edge (pass 2), or the lists-only draw filter
+// BsEmit for one slot of the edge (pass 2), or the lists-only draw filter.
+// Payload words are staged in the wave's LDS copy `w` (E.w points there) and
+// written to the entry by tri_flush: the many ORs into the same few words
+// (bitsets, Elias-Fano, draw filters) stay off the global atomic path.
 struct TriSlot {
   BsEmit E;
+  uint32_t* gw;  // the entry's payload words in HBM
   bool filt;  // lists-only build, region-size set: draw filter only
+  bool dual;  // dual list entry: the reverse slot's list goes to halfwords 6..11
   __device__ void operator()(int64_t k, uint32_t idx, int64_t kprev) const {
     if (filt)
       bs_filter_only(E.w, k, E.d);
@@ -307,25 +316,52 @@ struct TriSlot {
 };
 
 __device__ __forceinline__ TriSlot tri_slot(gw_bs_nbr* en, uint32_t* reg, const uint64_t* roff, int64_t e, uint32_t c,
-                                            uint32_t d, int lists_only) {
+                                            uint32_t d, int lists_only, uint32_t* stage, int lane) {
   TriSlot T;
   T.filt = lists_only && bs_mode(c, d) == BS_REGION;
+  T.dual = (en->meta & kMetaDual) != 0u;
   T.E = bs_emit(en, reg, roff, e, c, d);
+  T.gw = T.E.w;
+  T.E.w = stage;
+  if (T.E.pdir) T.E.pdir = reinterpret_cast<uint16_t*>(stage + 1);
+  if (lane < 12) stage[lane] = 0u;
+  __builtin_amdgcn_wave_barrier();
   return T;
 }
 
-// prologue of a slot's payload (pass 2): list padding, region block index
-__device__ __forceinline__ void tri_prologue(const TriSlot& T, int64_t e, uint32_t c, const uint64_t* roff, int lane) {
-  if (T.filt) return;
-  if (T.E.mode == BS_LIST && lane >= (int)c && lane < 2 * (int)gw_bs_pw(T.E.d))
-    reinterpret_cast<uint16_t*>(T.E.w)[lane] = 0xFFFFu;
-  if (T.E.mode == BS_REGION && lane == 0) T.E.w[0] = (uint32_t)(roff[e] / kBlk);
+// prologue of a slot's payload (pass 2, first chunk): region block index
+__device__ __forceinline__ void tri_prologue(const TriSlot& T, int64_t e, const uint64_t* roff, int lane) {
+  if (!T.filt && T.E.mode == BS_REGION && lane == 0) T.E.w[0] = (uint32_t)(roff[e] / kBlk);
 }
 
-// epilogue (pass 2): directory blocks after the last common position
-__device__ __forceinline__ void tri_epilogue(const TriSlot& T, int64_t klast, uint32_t c, int lane) {
-  if (T.filt || T.E.mode != BS_REGION) return;
+// epilogue (pass 2, last chunk): list padding, directory blocks after the last
+// common position; c_rev = the reverse slot's count (dual entries)
+__device__ __forceinline__ void tri_epilogue(const TriSlot& T, int64_t klast, uint32_t c, uint32_t c_rev, int lane) {
+  if (T.filt) return;
+  if (T.dual) {
+    if (lane < 2 * (int)kDualC && (lane < (int)kDualC ? lane >= (int)c : lane - (int)kDualC >= (int)c_rev))
+      reinterpret_cast<uint16_t*>(T.E.w)[lane] = 0xFFFFu;
+    return;
+  }
+  if (T.E.mode == BS_LIST && lane >= (int)c && lane < 2 * (int)gw_bs_pw(T.E.d))
+    reinterpret_cast<uint16_t*>(T.E.w)[lane] = 0xFFFFu;
+  if (T.E.mode != BS_REGION) return;
   for (int64_t g = (klast < 0 ? -1 : klast / kDirBits) + 1 + lane; g < T.E.ndir; g += 64) T.E.set_dir(g, g, c);
+}
+
+// staged payload words -> the entry (once per chunk; the entry's payload is
+// zero before the first flush, so later chunks OR into it)
+__device__ __forceinline__ void tri_flush(const TriSlot& T, bool merge, int lane) {
+  __builtin_amdgcn_wave_barrier();
+  const int pw = (int)gw_bs_pw(T.E.d);
+  if (lane < pw) {
+    const uint32_t v = T.E.w[lane];
+    if (!merge)
+      T.gw[lane] = v;
+    else if (v)
+      atomicOr(&T.gw[lane], v);
+  }
+  __builtin_amdgcn_wave_barrier();
 }
 
 __device__ __forceinline__ void tri_header(gw_bs_nbr* en, uint32_t x, uint32_t d, uint32_t off, uint32_t meta,
@@ -336,14 +372,21 @@ __device__ __forceinline__ void tri_header(gw_bs_nbr* en, uint32_t x, uint32_t d
 }
 
 // wave-level emission of this round's common positions of one slot: lanes
-// with `on` hold position pos; ranks continue from *cnt, kprev from *last
+// with `on` hold position pos; ranks continue from *cnt, kprev from *last;
+// rev (dual entries): the other slot's staged halfwords, whose reverse list
+// gets the same positions
 template <class F>
-__device__ __forceinline__ void tri_emit(const F& f, bool on, int64_t pos, uint32_t* cnt, int64_t* last, int lane) {
+__device__ __forceinline__ void tri_emit(const F& f, bool on, int64_t pos, uint32_t* cnt, int64_t* last, int lane,
+                                         uint16_t* rev) {
   const unsigned long long m = __ballot(on);
   if (!m) return;
   const unsigned long long lt = m & ((1ull << lane) - 1ull);
   const int64_t pin = __shfl(pos, lt ? 63 - __clzll(lt) : 0, 64);
-  if (on) f(pos, *cnt + (uint32_t)__popcll(lt), lt ? pin : *last);
+  if (on) {
+    const uint32_t idx = *cnt + (uint32_t)__popcll(lt);
+    f(pos, idx, lt ? pin : *last);
+    if (rev) rev[kDualC + idx] = (uint16_t)pos;
+  }
   *last = __shfl(pos, 63 - __clzll(m), 64);
   *cnt += (uint32_t)__popcll(m);
 }
@@ -352,7 +395,7 @@ __device__ __forceinline__ void tri_emit(const F& f, bool on, int64_t pos, uint3
 // blockIdx.x, blockIdx.x + gridDim.x, ...; hubs come first in the item order)
 template <bool FILL>
 __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* __restrict__ items, uint32_t nitems,
-                                                const uint8_t* __restrict__ loop, gw_bs_nbr* __restrict__ bsn,
+                                                gw_bs_nbr* __restrict__ bsn,
                                                 const uint64_t* __restrict__ roff, uint32_t* __restrict__ reg,
                                                 int lists_only) {
   __shared__ int32_t s_key[kTriS];
@@ -360,7 +403,14 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
   // per-edge state between chunks (hubs): common counts, last positions, kp(u -> v), cursor in N(v)
   __shared__ uint32_t s_cuv[kTriEB], s_cvu[kTriEB], s_cur[kTriEB];
   __shared__ int32_t s_luv[kTriEB], s_lvu[kTriEB], s_kp[kTriEB];
+  __shared__ uint32_t s_stage[kTW][2][12];  // pass 2: both slots' payload words, per wave
+  // pass 2: the (v -> u) slot's region bits of this chunk (positions p0 ..
+  // p0 + kTriH of N(u): one aligned window per chunk, written once)
+  __shared__ uint32_t s_win[kTW][kTriH / 32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (FILL) {
+    for (int i = lane; i < kTriH / 32; i += 64) s_win[wave][i] = 0u;
+  }
   for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
     if (item != blockIdx.x) __syncthreads();  // every wave is done with the previous item's hash and state
     const TriItem it = items[item];
@@ -373,7 +423,6 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
     while ((1 << lg) < 2 * hk) ++lg;
     const uint32_t S = 1u << lg, smask = S - 1u;
     const int sh = 32 - lg;
-    const bool u_loop = loop[u] != 0;
     for (int ch = 0; ch < nch; ++ch) {
       const int64_t p0 = (int64_t)ch * kTriH, p1 = min(du, p0 + kTriH);
       if (ch > 0) __syncthreads();  // every wave is done with the previous chunk
@@ -408,23 +457,32 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
         // pass 2: both slots' payload writers (headers from pass 1)
         TriSlot Tuv, Tvu;
         int64_t er = -1;
+        bool vu_win = false;
         if (FILL) {
           gw_bs_nbr* en = bsn + e;
           const uint32_t c = bs_c(en, (uint32_t)dv);
-          Tuv = tri_slot(en, reg, roff, e, c, (uint32_t)dv, lists_only);
-          if (ch == 0) tri_prologue(Tuv, e, c, roff, lane);
+          Tuv = tri_slot(en, reg, roff, e, c, (uint32_t)dv, lists_only, s_stage[wave][0], lane);
+          Tuv.E.nobits = true;  // (u -> v) positions are this round's lanes: whole bit words below
+          if (ch == 0) tri_prologue(Tuv, e, roff, lane);
           if (u != v) {
             const uint32_t kpv = (uint32_t)dv < GW_BS_PACK_D ? (en->r[0] & 0xFFFFu) : en->r[0];
             er = vb + kpv;  // the reverse slot (v -> u)
             gw_bs_nbr* enr = bsn + er;
             const uint32_t cr = bs_c(enr, (uint32_t)du);
-            Tvu = tri_slot(enr, reg, roff, er, cr, (uint32_t)du, lists_only);
-            if (ch == 0) tri_prologue(Tvu, er, cr, roff, lane);
+            Tvu = tri_slot(enr, reg, roff, er, cr, (uint32_t)du, lists_only, s_stage[wave][1], lane);
+            if (ch == 0) tri_prologue(Tvu, er, roff, lane);
+            vu_win = !Tvu.filt && Tvu.E.mode == BS_REGION;
+            Tvu.E.nobits = vu_win;  // region bits go through the LDS window
           }
         }
+        int64_t k = (int64_t)cur + lane;
+        int32_t x = k < dv ? G.nbrs[vb + k] : INT32_MAX;
         for (;;) {
-          const int64_t k = (int64_t)cur + lane;
-          const int32_t x = k < dv ? G.nbrs[vb + k] : INT32_MAX;
+          // the next round's elements are requested before this round is
+          // probed, so a wave keeps one row read in flight while it works (the
+          // extra read past the row's or the chunk's end costs one line)
+          const int64_t kn = k + 64;
+          const int32_t xn = kn < dv ? G.nbrs[vb + kn] : INT32_MAX;
           const bool inr = k < dv && x <= hi;
           bool hit = false;
           uint32_t pu = 0;
@@ -446,8 +504,24 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
           const bool cu = hit && x != u;              // (u -> v): position k in N(v)
           const bool cv = hit && x != v && u != v;    // (v -> u): position pu in N(u)
           if (FILL) {
-            tri_emit(Tuv, cu, k, &cuv, &luv, lane);
-            if (u != v) tri_emit(Tvu, cv, (int64_t)pu, &cvu, &lvu, lane);
+            if (!Tuv.filt && Tuv.E.mode == BS_REGION) {
+              // this round's positions are cur .. cur+63: its hits are whole
+              // words of the region bitset (at most three)
+              const unsigned long long m = __ballot(cu);
+              if (m) {
+                const uint32_t sh = cur & 31u;
+                const unsigned long long lo = m << sh;
+                const uint32_t hi3 = sh ? (uint32_t)(m >> (64 - sh)) : 0u;
+                const uint32_t wv = lane == 0 ? (uint32_t)lo : lane == 1 ? (uint32_t)(lo >> 32) : hi3;
+                if (lane < 3 && wv) atomicOr(&Tuv.E.bits[(cur >> 5) + lane], wv);
+              }
+            }
+            const bool dual = u != v && Tuv.dual;  // (both slots or neither)
+            tri_emit(Tuv, cu, k, &cuv, &luv, lane, dual ? reinterpret_cast<uint16_t*>(Tvu.E.w) : nullptr);
+            if (u != v) {
+              tri_emit(Tvu, cv, (int64_t)pu, &cvu, &lvu, lane, dual ? reinterpret_cast<uint16_t*>(Tuv.E.w) : nullptr);
+              if (cv && vu_win) atomicOr(&s_win[wave][(pu - (uint32_t)p0) >> 5], 1u << (pu & 31u));
+            }
           } else {
             const unsigned long long m1 = __ballot(cu), m2 = __ballot(cv);
             cuv += (uint32_t)__popcll(m1);
@@ -456,6 +530,27 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
           const int nin = __popcll(__ballot(inr));  // a prefix of the lanes (rows are sorted)
           cur += (uint32_t)nin;
           if (nin < 64) break;  // the chunk's id range or the row ended
+          k = kn;
+          x = xn;
+        }
+        if (FILL && ch + 1 == nch) {
+          tri_epilogue(Tuv, luv, cuv, cvu, lane);
+          if (u != v) tri_epilogue(Tvu, lvu, cvu, cuv, lane);
+        }
+        if (FILL) {
+          tri_flush(Tuv, nch > 1, lane);
+          if (u != v) tri_flush(Tvu, nch > 1, lane);
+          if (vu_win) {  // this chunk's window of (v -> u)'s region bits: plain stores, each word once
+            __builtin_amdgcn_wave_barrier();
+            for (int i = lane; i < kTriH / 32; i += 64) {
+              const uint32_t wv = s_win[wave][i];
+              if (wv) {
+                Tvu.E.bits[(p0 >> 5) + i] = wv;
+                s_win[wave][i] = 0u;
+              }
+            }
+            __builtin_amdgcn_wave_barrier();
+          }
         }
         if (ch + 1 < nch) {
           if (lane == 0) {
@@ -468,16 +563,14 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
           }
           continue;
         }
-        if (FILL) {
-          tri_epilogue(Tuv, luv, cuv, lane);
-          if (u != v) tri_epilogue(Tvu, lvu, cvu, lane);
-        } else {
+        if (!FILL) {
           const uint32_t k32 = kp >= 0 ? (uint32_t)kp : 0xFFFFFFFFu;
           if (lane == 0)
-            tri_header(bsn + e, (uint32_t)v, (uint32_t)dv, (uint32_t)vb, bs_meta_slot(cuv, (uint32_t)dv, u_loop), k32, cuv);
+            tri_header(bsn + e, (uint32_t)v, (uint32_t)dv, (uint32_t)vb,
+                       bs_meta_slot(cuv, u != v ? cvu : 0xFFFFu, (uint32_t)dv, (uint32_t)du), k32, cuv);
           if (lane == 1 && u != v && kp >= 0)
             tri_header(bsn + vb + kp, (uint32_t)u, (uint32_t)du, (uint32_t)ub,
-                       bs_meta_slot(cvu, (uint32_t)du, loop[v] != 0), (uint32_t)j, cvu);
+                       bs_meta_slot(cvu, cuv, (uint32_t)du, (uint32_t)dv), (uint32_t)j, cvu);
         }
       }
     }
@@ -553,11 +646,13 @@ __device__ __forceinline__ bool ef_bucket_has(const uint32_t (&pl)[kPW], uint32_
   return false;
 }
 
-// k in the inline common-neighbour list (registers, constant indices)
-__device__ __forceinline__ bool list_has(const uint32_t (&pl)[kPW], uint32_t k) {
+// k in the inline common-neighbour list (registers, constant indices); a
+// dual entry's own list is its first kDualC halfwords
+__device__ __forceinline__ bool list_has(const uint32_t (&pl)[kPW], uint32_t k, bool dual = false) {
   bool hit = false;
 #pragma unroll
-  for (int t = 0; t < kPW; ++t) hit |= (pl[t] & 0xFFFFu) == k || (pl[t] >> 16) == k;
+  for (int t = 0; t < kPW; ++t)
+    hit |= (t < (int)kDualC / 2 || !dual) && ((pl[t] & 0xFFFFu) == k || (pl[t] >> 16) == k);
   return hit;
 }
 
@@ -776,7 +871,7 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
           }
         } else if (op == 2) {
           if (mode == BS_LIST) {
-            common = c != 0u && list_has(pl, (uint32_t)k);  // c == 0: pl may hold the return stash
+            common = c != 0u && list_has(pl, (uint32_t)k, (meta & kMetaDual) != 0u);
           } else if (mode == BS_INLINE) {
             common = win & 1u;
           } else if (mode == BS_EF) {
@@ -798,10 +893,10 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
         isblk = true;
       }
       if (acc) {
-        if (meta == kMetaStash && k == (int64_t)kp) {
-          // return over an edge with no common neighbours: the entry of the
-          // reverse slot (cur -> prev) is {prev, its degree and row, kp = the
-          // index drawn at prev, c = 0, empty list}, all kept in pl[0..3]
+        if ((meta & kMetaStash) && k == (int64_t)kp) {
+          // return over a dual entry's edge: the entry of the reverse slot
+          // (cur -> prev) is {prev, its degree and row, kp = the index drawn
+          // at prev (stash, pl[6..9]), its list (pl[3..5]) and count}
           virt = true;
         } else {
           slot = b + (uint32_t)k;
@@ -850,27 +945,35 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
       b = E[2];
       meta = E[3];
       unpack_entry(E, &kp, &c, pl);
-      if (meta == kMetaStashOk && od < GW_BS_PACK_D) {
-        // empty list (and c(cur -> ou) = 0 too): its payload words keep the
-        // row we came from (a later return needs no fetch); kMetaStash marks
-        // the stash (list mode)
-        pl[0] = ou;
-        pl[1] = od;
-        pl[2] = ob;
-        pl[3] = ok;
-        meta = kMetaStash;
+      if (meta & kMetaDual) {
+        // dual list entry (both degrees < 65536): its payload words 6..9
+        // keep the row we came from, so a return needs no fetch
+        pl[6] = ou;
+        pl[7] = od;
+        pl[8] = ob;
+        pl[9] = ok;
+        meta |= kMetaStash;
       }
     }
-    if (virt) {  // swap the current row and the stash: the walker is back at prev
+    if (virt) {  // the walker is back at prev: swap rows, lists and counts
       const uint32_t tc = (uint32_t)cur, td = d, tb = b, tk = kp;
-      cur = (int32_t)pl[0];
-      d = pl[1];
-      b = pl[2];
-      kp = pl[3];
-      pl[0] = tc;
-      pl[1] = td;
-      pl[2] = tb;
-      pl[3] = tk;
+      cur = (int32_t)pl[6];
+      d = pl[7];
+      b = pl[8];
+      kp = pl[9];
+      pl[6] = tc;
+      pl[7] = td;
+      pl[8] = tb;
+      pl[9] = tk;
+#pragma unroll
+      for (int q = 0; q < (int)kDualC / 2; ++q) {
+        const uint32_t t = pl[q];
+        pl[q] = pl[q + kDualC / 2];
+        pl[q + kDualC / 2] = t;
+      }
+      const uint32_t c_rev = (meta >> 2) & 7u;
+      meta = kMetaDual | kMetaStash | (c << 2);
+      c = c_rev;
     }
     const bool moved = slot != 0xFFFFFFFFu || virt;
     if (moved) {
@@ -957,7 +1060,7 @@ struct LsParams {
 __device__ __forceinline__ bool payload_has(const uint32_t (&pl)[kPW], uint32_t meta, uint32_t c, uint32_t k) {
   const uint32_t mode = meta & 3u;
   const uint32_t efl = (meta >> 2) & 31u, efU = (meta >> 7) & 511u;
-  if (mode == BS_LIST) return list_has(pl, k);
+  if (mode == BS_LIST) return list_has(pl, k, (meta & 0x8000u) != 0u);  // bit 15: dual entry
   const uint32_t eh = k >> efl;
   uint32_t es = 0;
   if (mode == BS_EF && eh > 0) {  // bucket eh starts after the (eh-1)-th zero of the high parts
@@ -1119,7 +1222,7 @@ k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t wal
       unpack_entry(E, &ekp, &ec, pl);
       pdx = E[1];
       poff = E[2];
-      pmeta = (E[3] & 0xFFFFu) | (min(ec, 0xFFFFu) << 16);
+      pmeta = (E[3] & 0x7FFFu) | ((E[3] & kMetaDual) ? 0x8000u : 0u) | (min(ec, 0xFFFFu) << 16);
     }
     bool ready = false;
     int flen = 0;
@@ -1262,7 +1365,6 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
   int rc;
   uint64_t* sz = nullptr;
   uint64_t* roff = nullptr;
-  uint8_t* loop = nullptr;
   int32_t *ids = nullptr, *order = nullptr;
   uint32_t* nit = nullptr;
   uint32_t* itoff = nullptr;
@@ -1271,7 +1373,6 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
   auto cleanup = [&]() {
     bs_free(sz);
     bs_free(roff);
-    bs_free(loop);
     bs_free(ids);
     bs_free(order);
     bs_free(nit);
@@ -1292,12 +1393,11 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
       return fail(GW_ERR_DEVICE);                                    \
     }                                                                \
   } while (0)
-  if ((rc = bs_alloc(g, &d.bs_nbr, nnz)) || (rc = bs_alloc(g, &loop, n)) || (rc = bs_alloc(g, &ids, n)) ||
+  if ((rc = bs_alloc(g, &d.bs_nbr, nnz)) || (rc = bs_alloc(g, &ids, n)) ||
       (rc = bs_alloc(g, &order, n)) || (rc = bs_alloc(g, &nit, n + 1)) || (rc = bs_alloc(g, &itoff, n + 1)))
     return fail(rc);
   const unsigned gn = (unsigned)((n + kB - 1) / kB), gn1 = (unsigned)((n + 1 + kB - 1) / kB);
   BS_TRY(hipMemset(d.bs_nbr, 0, (size_t)nnz * sizeof(gw_bs_nbr)));
-  k_bs_selfloop<<<gn, kB>>>(d, loop);
   k_bs_iota<<<gn, kB>>>(n, ids);
   BS_TRY(hipGetLastError());
   // work items: vertices by degree, descending (hubs first), kTriEB edges each
@@ -1325,7 +1425,7 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
   bs_free(itoff);
   // pass 1: headers
   const unsigned tgrid = std::min<uint32_t>(nitems, 1u << 20);  // <= 2^29 work-items per launch
-  if (nitems) k_bs_tri<false><<<tgrid, kTB>>>(d, items, nitems, loop, d.bs_nbr, nullptr, nullptr, lists_only ? 1 : 0);
+  if (nitems) k_bs_tri<false><<<tgrid, kTB>>>(d, items, nitems, d.bs_nbr, nullptr, nullptr, lists_only ? 1 : 0);
   BS_TRY(hipGetLastError());
   // region layout
   if ((rc = bs_alloc(g, &sz, nnz + 1)) || (rc = bs_alloc(g, &roff, nnz + 1))) return fail(rc);
@@ -1353,7 +1453,7 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
   BS_TRY(hipMemset(d.bs_region, 0, (size_t)words * 4));
   // pass 2: payloads
   if (nitems)
-    k_bs_tri<true><<<tgrid, kTB>>>(d, items, nitems, loop, d.bs_nbr, roff, d.bs_region, lists_only ? 1 : 0);
+    k_bs_tri<true><<<tgrid, kTB>>>(d, items, nitems, d.bs_nbr, roff, d.bs_region, lists_only ? 1 : 0);
   BS_TRY(hipGetLastError());
   BS_TRY(hipDeviceSynchronize());
 #undef BS_TRY

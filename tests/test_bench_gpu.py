@@ -55,3 +55,29 @@ def test_bench_config4_shape_small():
     assert rc == 0, err[-3000:]
     assert res["sampler"] == "rejection" and res["config"]["baseline_config"] == 4
     assert res["value"] > 0 and 1.0 <= res["rejection_trials_per_step"] < 3.0
+
+
+@pytest.mark.gpu
+def test_bench_config4_strong_two_ranks_gloo_on_gpu():
+    """Config 4's BASELINE shape with real walks: the fixed r=10 workload
+    split over 2 ranks (strong scaling), then all-gathered; the last rank's
+    gathered block equals rank 0's own recomputation of it."""
+    rc, res, err = _run(["--gpus", "2", "--config", "4"] + SMALL, {"GW_DIST_BACKEND": "gloo"})
+    assert rc == 0, err[-3000:]
+    assert res["scaling"] == "strong" and res["ranks"] == 2
+    total = res["config"]["walks_per_step"]
+    assert res["walk_steps"] <= 2 * total * 79 and res["walk_steps"] > 0
+    assert res["allgather"]["check_last_rank_block_identical"] is True and res["allgather_all_ranks_ok"] is True
+    assert res["end_to_end"]["prepare_s"] >= 0 and res["end_to_end"]["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_config5_two_ranks_rows_allgather_gloo_on_gpu():
+    """Config 5 (TopSim top-100) on a 200k-vertex Java R-MAT over 2 ranks: the
+    round-robin source shards' rows all-gathered, blocks checked against the
+    senders' checksums."""
+    rc, res, err = _run(["--gpus", "2", "--config", "5", "--p10m-vertices", "200000", "--no-cpu-baseline"],
+                        {"GW_DIST_BACKEND": "gloo"})
+    assert rc == 0, err[-3000:]
+    assert res["scaling"] == "strong" and res["ranks"] == 2 and res["value"] > 0
+    assert res["allgather"]["check_blocks_match_sender_checksums"] is True
