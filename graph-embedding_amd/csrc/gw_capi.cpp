@@ -235,6 +235,8 @@ int gw_graph_info(const gw_graph* g, gw_graph_info_t* info) {
   info->sampler_bytes = (g->d.bs_nbr ? g->bitset_words * 4 + g->nnz * (int64_t)sizeof(gw_bs_nbr) : 0) +
                         (g->d.sent ? g->nnz * (int64_t)sizeof(gw_ts_ent) : 0) +
                         (g->d.eh ? 2 * g->nnz * (int64_t)sizeof(int32_t) : 0);
+  info->n2v_mode = g->n2v_prepared ? g->n2v_mode : -1;
+  info->listed = (g->n2v_prepared && g->n2v_mode == GW_N2V_REJECTION && g->d.bs_nbr) ? 1 : 0;
   return GW_OK;
 }
 
@@ -293,7 +295,7 @@ int gw_n2v_prepare(gw_graph* g, double p, double q, int mode) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
   GW_GUARD_DEVICE(g, g->device);
   if (!(p > 0) || !(q > 0)) return ret(g, gw_fail(g, GW_ERR_ZERODIV, "p and q must be > 0 (node2vec.py:70-76 divides by them)"));
-  if (mode != GW_N2V_REPLAY && mode != GW_N2V_REJECTION && mode != GW_N2V_BITSET)
+  if (mode != GW_N2V_REPLAY && mode != GW_N2V_REJECTION && mode != GW_N2V_BITSET && mode != GW_N2V_AUTO)
     return ret(g, gw_fail(g, GW_ERR_INVALID, "unknown mode %d", mode));
   if (mode == GW_N2V_BITSET && (g->weighted || g->directed || g->semantics != GW_SEM_NX_SIMPLE))
     return ret(g, gw_fail(g, GW_ERR_UNSUPPORTED, "GW_N2V_BITSET needs an unweighted undirected NX_SIMPLE graph"));

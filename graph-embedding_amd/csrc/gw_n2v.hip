@@ -597,14 +597,71 @@ static int64_t table_budget(gw_graph* g) {
 // 1.60 -> 1.14 requests/step at ~4.9e10 requests/s) but cost an
 // edge-centric common-neighbour build; with expected_steps known, build them
 // only when the modelled build time is paid back.
-static bool listed_pays(gw_graph* g) {
+static bool listed_pays(gw_graph* g, double q) {
   if (g->opt.listed == 0) return false;
   if (g->opt.listed == 1 || g->opt.expected_steps <= 0) return true;
+  // the payload answers has_edge probes; with q >= 1 the candidates' own
+  // entry reads dominate and listed entries measure no faster (R-MAT-20,
+  // p = 0.25, q = 4: 53.0 vs 52.6 ms per 5.1e8 steps)
+  if (q >= 1.0) return false;
   const double save_s = (double)g->opt.expected_steps * (0.46 / 4.9e10);
   return save_s > gw_bitset_build_model_s(g);
 }
 
+// bitset walk time per step (R-MAT-20 headline 3.2e10 walk-steps/s) and the
+// rejection sampler's time per trial (see n2v_prepare_auto)
+constexpr double kBitsetStepSeconds = 1.0 / 3.2e10;
+constexpr double kRejTrialSeconds = 3.7e-11;
+
+// GW_N2V_AUTO: see include/graphwalk.h
+static int n2v_prepare_auto(gw_graph* g, double p, double q) {
+  const bool bs_ok = !g->weighted && !g->directed && g->semantics == GW_SEM_NX_SIMPLE && !(p == 1.0 && q == 1.0) &&
+                     g->nnz > 0 && g->nnz < (int64_t)0xFFFFFFFF;
+  auto bitset_or_rejection = [&]() {
+    int rc = gw_dev_n2v_prepare(g, p, q, GW_N2V_BITSET);
+    if (rc == GW_ERR_CAPACITY || rc == GW_ERR_NOMEM) {
+      (void)hipGetLastError();
+      g->err.clear();
+      rc = gw_dev_n2v_prepare(g, p, q, GW_N2V_REJECTION);
+    }
+    return rc;
+  };
+  if (!bs_ok) return gw_dev_n2v_prepare(g, p, q, GW_N2V_REJECTION);
+  const int64_t steps = g->opt.expected_steps;
+  if (steps <= 0) return bitset_or_rejection();
+  int rc = gw_dev_n2v_prepare(g, p, q, GW_N2V_REJECTION);
+  if (rc != GW_OK) return rc;
+  // pilot: the rejection sampler's own walks (65,536 walks of length 80 from
+  // iteration 0's shuffled starts, a fixed internal seed) counting its trials
+  // per step; the modelled time per trial is measured (R-MAT-20 p = 0.25
+  // q = 4: 3.06 trials/step, 52.6 ms per 5.1e8 steps; R-MAT-24 p = 1 q = 0.5:
+  // 1.03, 286 ms per 7.0e9).  Counting, not timing, keeps the choice (and so
+  // the walks) a function of the inputs.
+  const int64_t pw = std::min<int64_t>(65536, std::max<int64_t>(g->n, 1));
+  const int L = 80;
+  int32_t* buf = nullptr;
+  uint64_t* cnt = nullptr;
+  double t_rej = -1.0;
+  if (dev_alloc(g, &buf, pw * L) == GW_OK && dev_alloc(g, &cnt, 2) == GW_OK) {
+    uint64_t h[2] = {0, 0};
+    const bool ok = hipMemset(cnt, 0, 2 * sizeof(uint64_t)) == hipSuccess &&
+                    gw_dev_n2v_walks(g, L, 0x5eedull, 0, pw, 1, buf, nullptr, cnt, nullptr) == GW_OK &&
+                    hipMemcpy(h, cnt, sizeof h, hipMemcpyDeviceToHost) == hipSuccess;
+    if (ok && h[0] > 0) t_rej = (double)h[1] / (double)h[0] * kRejTrialSeconds;
+  }
+  dev_free(buf);
+  dev_free(cnt);
+  (void)hipGetLastError();
+  if (t_rej < 0) return GW_OK;  // no pilot: keep the rejection sampler
+  const double build = gw_bitset_build_model_s(g);
+  const double bitset_s = build + (double)steps * kBitsetStepSeconds;
+  const double rejection_s = (double)steps * t_rej;
+  if (build < 0 || bitset_s >= rejection_s) return GW_OK;
+  return bitset_or_rejection();
+}
+
 int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
+  if (mode == GW_N2V_AUTO) return n2v_prepare_auto(g, p, q);
   if (g->device < 0) {
     g->err = "graph is not on a device (call gw_graph_to_device)";
     return GW_ERR_STATE;
@@ -702,7 +759,7 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
   // HBM, < 2^32 slots) the 16 B slot entries below serve k_walk_scale
   bool listed = false;
   if (mode == GW_N2V_REJECTION && !fo && g->nnz && !g->weighted && !g->directed &&
-      g->semantics == GW_SEM_NX_SIMPLE && !GW_DIAG_ENV("GW_DIAG_NO_LISTS") && listed_pays(g)) {
+      g->semantics == GW_SEM_NX_SIMPLE && !GW_DIAG_ENV("GW_DIAG_NO_LISTS") && listed_pays(g, q)) {
     rc = gw_dev_bitset_build(g, table_budget(g), true);
     if (rc == GW_OK) {
       listed = true;

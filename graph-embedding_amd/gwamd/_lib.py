@@ -37,6 +37,7 @@ SEM_JAVA_MULTI = 1
 N2V_REPLAY = 0
 N2V_REJECTION = 1
 N2V_BITSET = 2
+N2V_AUTO = 3
 TOPSIM_SINGLE_SAMPLE = 0
 TOPSIM_ENUMERATE = 1
 TOPSIM_SINGLE_RW = 2
@@ -72,7 +73,7 @@ class GraphInfo(ctypes.Structure):
                 ("max_degree", ctypes.c_int64), ("edge_alias_entries", ctypes.c_int64),
                 ("semantics", ctypes.c_int32), ("directed", ctypes.c_int32),
                 ("weighted", ctypes.c_int32), ("device", ctypes.c_int32),
-                ("sampler_bytes", ctypes.c_int64)]
+                ("sampler_bytes", ctypes.c_int64), ("n2v_mode", ctypes.c_int32), ("listed", ctypes.c_int32)]
 
 
 class Options(ctypes.Structure):

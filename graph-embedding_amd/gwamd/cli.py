@@ -14,8 +14,10 @@ save_list format (DeepSim/src/main.py:237-243) or as .npy.
 --mode replay : reference-exact (networkx graph, global random/np.random
                 seeded with --seed, per-edge alias tables on the GPU);
 --mode scale  : Philox samplers (any size; identical for any GPU count):
-                --sampler auto picks the per-edge bitset sampler when its
-                tables fit (unweighted undirected graphs), else rejection.
+                --sampler auto (GW_N2V_AUTO) picks the per-edge bitset
+                sampler or the rejection sampler by modelled end-to-end
+                time for this run's walks (a one-pass run on R-MAT-20:
+                rejection, 0.05 s vs 0.22 s, the bitset build dominating).
 
 Multi-GPU (scale mode): launch one process per GPU with torchrun; rank r
 walks its contiguous block of the global walk indices on GPU LOCAL_RANK, the
@@ -102,16 +104,23 @@ def _scale(args):
     # the walks this rank will run on this preparation: the sampler's optional
     # tables are built only when they pay back within them (gw_options_t)
     g.options(expected_steps=gd.shard_range(args.num_walks * g.n, world, rank)[1] * (args.walk_length - 1))
-    mode = C.N2V_REJECTION
-    if args.sampler != "rejection" and not args.directed and not args.weighted and (args.p, args.q) != (1.0, 1.0):
-        try:
-            C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, C.N2V_BITSET), g.handle)
-            mode = C.N2V_BITSET
-        except C.CapacityError:
-            if args.sampler == "bitset":
-                raise
-    if mode == C.N2V_REJECTION:
-        C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, C.N2V_REJECTION), g.handle)
+    if args.sampler == "auto":
+        # the library picks bitset or rejection by modelled end-to-end time for
+        # the walks announced above (the rejection sampler's pilot trials
+        # against the bitset build model); with several ranks rank 0 decides
+        # for all, so every shard comes from the same sampler
+        if world == 1 or rank == 0:
+            C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, C.N2V_AUTO), g.handle)
+        if world > 1:
+            import torch.distributed as dist
+            dev = torch.device("cuda", device) if args.dist_backend == "nccl" else torch.device("cpu")
+            m = torch.tensor([g.info().n2v_mode if rank == 0 else -1], dtype=torch.int64, device=dev)
+            dist.broadcast(m, 0)
+            if rank != 0:
+                C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, int(m.item())), g.handle)
+    else:
+        mode = C.N2V_BITSET if args.sampler == "bitset" else C.N2V_REJECTION
+        C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, mode), g.handle)
     nwalks = args.num_walks * g.n
     L = args.walk_length
     begin, count = gd.shard_range(nwalks, world, rank)

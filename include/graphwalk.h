@@ -83,6 +83,16 @@ extern "C" {
  * (return / common neighbour / other) with no has_edge probes.  Philox keyed
  * like GW_N2V_REJECTION.                                                   */
 #define GW_N2V_BITSET 2
+/* pick BITSET or REJECTION by modelled end-to-end time (prepare + the walk
+ * steps announced in gw_options_t.expected_steps): the rejection sampler is
+ * prepared (milliseconds) and a pilot of its walks counts its trials per
+ * step (time = trials x a measured cost per trial); the bitset sampler's
+ * time is its build model (sum over edges of min(deg u, deg v)) plus the
+ * steps at its measured rate.  The choice is a function of the graph, p, q
+ * and expected_steps (no timing), so runs repeat.  With expected_steps = 0
+ * (unknown) the bitset sampler is taken whenever it applies and fits (the
+ * throughput choice).  gw_graph_info().n2v_mode reports the choice.       */
+#define GW_N2V_AUTO 3
 
 /* ---- TopSim variants (DeepSim/TopSimAll/src/simrank/) --------------------- */
 #define GW_TOPSIM_SINGLE_SAMPLE 0 /* TopSim_singleSample.java:62-203 (= _Basic) */
@@ -102,6 +112,8 @@ typedef struct gw_graph_info_t {
   int32_t device;     /* -1 when not resident                               */
   int64_t sampler_bytes; /* HBM held by the prepared n2v sampler's per-slot tables
                             (bitset entries + regions, or rejection slot entries) */
+  int32_t n2v_mode;   /* GW_N2V_* the last gw_n2v_prepare built (-1: none)    */
+  int32_t listed;     /* 1: the rejection sampler has 64 B listed entries      */
 } gw_graph_info_t;
 
 /* Per-handle tuning (gw_graph_set_options).  Sizes and sampler choices

@@ -640,3 +640,33 @@ def test_replay_sink_heavy_directed_many_walks(gw, oracle):
     assert used.value == rused
     assert dt < 20.0, dt
     del inf
+
+
+def test_auto_sampler_choice_by_end_to_end_model(gw):
+    """GW_N2V_AUTO: with the walk steps announced (gw_options_t.expected_steps)
+    the library takes the rejection sampler when the bitset build cannot pay
+    back and the bitset sampler when it can; unknown steps (0) keep the
+    throughput choice (bitset); weighted graphs always take rejection; the
+    choice is deterministic (pilot trials are counted, not timed)."""
+    from gwamd import _lib as C
+    G = gw.GWGraph.rmat(17, 16, seed=5).to_device(0)
+    picks = []
+    for steps in (0, 10**6, 10**13, 10**6):
+        G.options(expected_steps=steps)
+        C.check(C.lib().gw_n2v_prepare(G.handle, 0.25, 4.0, C.N2V_AUTO), G.handle)
+        picks.append(G.info().n2v_mode)
+    assert picks == [C.N2V_BITSET, C.N2V_REJECTION, C.N2V_BITSET, C.N2V_REJECTION], picks
+    W = gw.GWGraph.from_edgelist(os.path.join(DATA, "weighted_quirks.edgelist"), " ", "nx", False, True).to_device(0)
+    W.options(expected_steps=10**13)
+    C.check(C.lib().gw_n2v_prepare(W.handle, 0.5, 2.0, C.N2V_AUTO), W.handle)
+    assert W.info().n2v_mode == C.N2V_REJECTION
+    # listed entries: never for q >= 1 under a known step count, on for q < 1 when they pay back
+    G.options(expected_steps=10**6, listed=-1)
+    C.check(C.lib().gw_n2v_prepare(G.handle, 1.0, 0.5, C.N2V_REJECTION), G.handle)
+    assert G.info().listed == 0
+    G.options(expected_steps=10**14)
+    C.check(C.lib().gw_n2v_prepare(G.handle, 1.0, 0.5, C.N2V_REJECTION), G.handle)
+    assert G.info().listed == 1
+    G.options(expected_steps=10**14)
+    C.check(C.lib().gw_n2v_prepare(G.handle, 0.25, 4.0, C.N2V_REJECTION), G.handle)
+    assert G.info().listed == 0

@@ -28,7 +28,9 @@ sys.path.insert(0, os.path.join(ROOT, "graph-embedding_amd"))
 def load(path, C):
     L = ctypes.CDLL(path)
     for name, (res, args) in C.SIGNATURES.items():
-        f = getattr(L, name)
+        f = getattr(L, name, None)  # older builds (tools/build_rev_lib.sh) lack newer entry points
+        if f is None:
+            continue
         f.restype = res
         f.argtypes = args
     return L
@@ -54,7 +56,10 @@ def main():
         if x in ("main", "diag"):
             return os.path.join(ROOT, "graph-embedding_amd", "gwamd",
                                 "libgraphwalk.so" if x == "main" else "libgraphwalk_diag.so")
-        return x if os.path.sep in x else os.path.join(ROOT, "abl", x + ".so")
+        if os.path.sep in x:
+            return x
+        ab = os.path.join(ROOT, "graph-embedding_amd", "gwamd", "ab", "libgraphwalk_" + x + ".so")
+        return ab if os.path.exists(ab) else os.path.join(ROOT, "abl", x + ".so")
     envs = [dict([x.split(":", 1)[1].split("=", 1)]) if ":" in x else {} for x in a.libs]
     paths = [path_of(x) for x in a.libs]
     libs = [load(p, C) for p in paths]

@@ -64,13 +64,13 @@ def main():
             if a.walks and ts[-1] is not None:
                 # one BASELINE pass: `walks` walks from every vertex, L = 80 (launched twice, second timed)
                 nw, L = a.walks * inf.n, 80
-                out = torch.empty((nw, L), dtype=torch.int32, device="cuda")
+                wbuf = torch.empty((nw, L), dtype=torch.int32, device="cuda")
                 cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
                 for rep in range(2):
                     cnt.zero_()
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
-                    C.check(C.lib().gw_n2v_walks(G.handle, L, 42, 0, nw, 1, C.ptr(out), None, C.ptr(cnt), None),
+                    C.check(C.lib().gw_n2v_walks(G.handle, L, 42, 0, nw, 1, C.ptr(wbuf), None, C.ptr(cnt), None),
                             G.handle)
                     e1.record()
                     torch.cuda.synchronize()
@@ -79,7 +79,7 @@ def main():
                 res[mode + "_walk_s"] = ws
                 res[mode + "_walk_steps_per_s"] = steps / ws
                 res[mode + "_end_to_end_s"] = ts[-1] + ws
-                del out
+                del wbuf
                 print(f"[walk] {name} {mode}: {ws * 1e3:.1f} ms, {steps / ws:.3e} steps/s, "
                       f"e2e {ts[-1] + ws:.3f} s", file=sys.stderr, flush=True)
             print(f"[build] {name} {mode}: {ts}", file=sys.stderr, flush=True)
