@@ -46,6 +46,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 #include "gw_device_common.h"
@@ -123,13 +124,39 @@ __device__ __forceinline__ int word_select(uint32_t x, uint32_t j) {
 enum { BS_LIST = 0, BS_INLINE = 1, BS_EF = 2, BS_REGION = 3 };
 constexpr uint32_t kFiltL = 320;  // lists-only builds: a region-size common set leaves a 320-bucket draw filter
 
+// The 32-bit draw words y whose index floor(y * d / 2^32) is k are
+// [floor(k * 2^32 / d), ceil((k + 1) * 2^32 / d) - 1].  Both ends come from
+// inv = 2^32 / d in double precision (k * inv is within 2^-20 of the quotient,
+// k <= d < 2^31) and one integer correction, instead of two 64-bit divisions
+// per common position.
+__device__ __forceinline__ int64_t bs_div32(int64_t k, uint32_t d, double inv, bool* exact) {
+  int64_t q = (int64_t)((double)k * inv);
+  int64_t r = (k << 32) - q * (int64_t)d;
+  if (r < 0) {
+    --q;
+    r += d;
+  } else if (r >= (int64_t)d) {
+    ++q;
+    r -= d;
+  }
+  *exact = r == 0;
+  return q;
+}
+__device__ __forceinline__ void bs_draw_range(int64_t k, uint32_t d, double inv, uint32_t* ylo, uint32_t* yhi) {
+  bool ex;
+  *ylo = (uint32_t)bs_div32(k, d, inv, &ex);
+  const int64_t q1 = bs_div32(k + 1, d, inv, &ex);
+  *yhi = (uint32_t)(q1 - (ex ? 1 : 0));
+}
+__device__ __forceinline__ double bs_inv32(uint32_t d) { return 4294967296.0 / (double)d; }
+
 // lists-only builds (k_walk_listed): for common position k of a slot whose
 // set needs a region, set the filter buckets of every draw (hi : lo) with
 // index k, bucket = hi * kFiltL >> 32 (the listed draw's high word is u.x)
-__device__ __forceinline__ void bs_filter_only(uint32_t* w, int64_t k, uint32_t d) {
-  const uint64_t ulo = ((uint64_t)k << 32) / d;
-  const uint64_t uhi = ((((uint64_t)k + 1) << 32) + d - 1) / d - 1;
-  const uint32_t b0 = (uint32_t)((ulo * kFiltL) >> 32), b1 = (uint32_t)((uhi * kFiltL) >> 32);
+__device__ __forceinline__ void bs_filter_only(uint32_t* w, int64_t k, uint32_t d, double inv) {
+  uint32_t ulo, uhi;
+  bs_draw_range(k, d, inv, &ulo, &uhi);
+  const uint32_t b0 = gw_bounded(ulo, kFiltL), b1 = gw_bounded(uhi, kFiltL);
   for (uint32_t b = b0; b <= b1; ++b) atomicOr(&w[b >> 5], 1u << (b & 31));
 }
 __device__ __forceinline__ int bs_mode(uint32_t c, uint32_t d) {
@@ -182,6 +209,7 @@ struct BsEmit {
   uint32_t* bits;  // region bits
   int64_t ndir;
   uint32_t d;
+  double inv;  // 2^32 / d (region filters)
   int l;
   uint32_t U;
   __device__ void operator()(int64_t k, uint32_t idx, int64_t kprev) const {
@@ -203,10 +231,10 @@ struct BsEmit {
       set_dir((kprev < 0 ? -1 : kprev / kDirBits) + 1, k / kDirBits, idx);
       // filter over the draw's high word y (bucket floor(y*F / 2^32)): the 64-bit draws
       // (y:z) with index k have y in [floor(k*2^32/d), ceil((k+1)*2^32/d) - 1]
-      const uint64_t ulo = ((uint64_t)k << 32) / d;
-      const uint64_t uhi = ((((uint64_t)k + 1) << 32) + d - 1) / d - 1;
+      uint32_t ulo, uhi;
+      bs_draw_range(k, d, inv, &ulo, &uhi);
       const uint32_t F = bs_filt_buckets(ndir, d), w0 = bs_filt_word(ndir);
-      const uint32_t b0 = gw_bounded((uint32_t)ulo, F), b1 = gw_bounded((uint32_t)uhi, F);
+      const uint32_t b0 = gw_bounded(ulo, F), b1 = gw_bounded(uhi, F);
       for (uint32_t b = b0; b <= b1; ++b) atomicOr(&w[w0 + (b >> 5)], 1u << (b & 31));
     }
   }
@@ -236,6 +264,7 @@ __device__ __forceinline__ BsEmit bs_emit(gw_bs_nbr* en, uint32_t* reg, const ui
   E.dir = E.bits = nullptr;
   E.pdir = nullptr;
   E.d = d;
+  E.inv = bs_inv32(d);
   E.l = 0;
   E.U = 0;
   if (E.mode == BS_EF) {
@@ -310,7 +339,7 @@ struct TriSlot {
   bool dual;  // dual list entry: the reverse slot's list goes to halfwords 6..11
   __device__ void operator()(int64_t k, uint32_t idx, int64_t kprev) const {
     if (filt)
-      bs_filter_only(E.w, k, E.d);
+      bs_filter_only(E.w, k, E.d, E.inv);
     else
       E(k, idx, kprev);
   }
@@ -376,19 +405,26 @@ __device__ __forceinline__ void tri_header(gw_bs_nbr* en, uint32_t x, uint32_t d
 // with `on` hold position pos; ranks continue from *cnt, kprev from *last;
 // rev (dual entries): the other slot's staged halfwords, whose reverse list
 // gets the same positions
+// (positions < 2^31; the previous position is only needed by region slots'
+// directories, and the round's last one and the count are wave-uniform)
 template <class F>
 __device__ __forceinline__ void tri_emit(const F& f, bool on, int64_t pos, uint32_t* cnt, int64_t* last, int lane,
-                                         uint16_t* rev) {
+                                         uint16_t* rev, bool need_prev) {
   const unsigned long long m = __ballot(on);
   if (!m) return;
   const unsigned long long lt = m & ((1ull << lane) - 1ull);
-  const int64_t pin = __shfl(pos, lt ? 63 - __clzll(lt) : 0, 64);
+  const int32_t p32 = (int32_t)pos;
+  int64_t prev = *last;
+  if (need_prev) {
+    const int32_t pin = __shfl(p32, lt ? 63 - __clzll(lt) : 0, 64);
+    if (lt) prev = pin;
+  }
   if (on) {
     const uint32_t idx = *cnt + (uint32_t)__popcll(lt);
-    f(pos, idx, lt ? pin : *last);
+    f(pos, idx, prev);
     if (rev) rev[kDualC + idx] = (uint16_t)pos;
   }
-  *last = __shfl(pos, 63 - __clzll(m), 64);
+  *last = __builtin_amdgcn_readlane(p32, 63 - __clzll(m));
   *cnt += (uint32_t)__popcll(m);
 }
 
@@ -409,6 +445,10 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
   // p0 + kTriH of N(u): one aligned window per chunk, written once)
   __shared__ uint32_t s_win[kTW][kTriH / 32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // diagnostics build only (GW_DIAG_BS_FILL, timing experiments, wrong tables):
+  // 1 = no payload emission, 2 = no region-bit stores, 4 = no payload flush
+  const int diag = kGwDiag ? (lists_only >> 8) : 0;
+  lists_only &= 1;
   if (FILL) {
     for (int i = lane; i < kTriH / 32; i += 64) s_win[wave][i] = 0u;
   }
@@ -455,6 +495,10 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
           lvu = s_lvu[li];
           kp = s_kp[li];
         }
+        // the first round's elements are requested before pass 2's header
+        // reads, so the two latencies overlap
+        int64_t k = (int64_t)cur + lane;
+        int32_t x = k < dv ? G.nbrs[vb + k] : INT32_MAX;
         // pass 2: both slots' payload writers (headers from pass 1)
         TriSlot Tuv, Tvu;
         int64_t er = -1;
@@ -476,8 +520,6 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
             Tvu.E.nobits = vu_win;  // region bits go through the LDS window
           }
         }
-        int64_t k = (int64_t)cur + lane;
-        int32_t x = k < dv ? G.nbrs[vb + k] : INT32_MAX;
         for (;;) {
           // the next round's elements are requested before this round is
           // probed, so a wave keeps one row read in flight while it works (the
@@ -504,8 +546,8 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
           if (mu) kp = (int64_t)cur + (__ffsll(mu) - 1);
           const bool cu = hit && x != u;              // (u -> v): position k in N(v)
           const bool cv = hit && x != v && u != v;    // (v -> u): position pu in N(u)
-          if (FILL) {
-            if (!Tuv.filt && Tuv.E.mode == BS_REGION) {
+          if (FILL && !(diag & 1)) {
+            if (!(diag & 2) && !Tuv.filt && Tuv.E.mode == BS_REGION) {
               // this round's positions are cur .. cur+63: its hits are whole
               // words of the region bitset (at most three)
               const unsigned long long m = __ballot(cu);
@@ -518,12 +560,14 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
               }
             }
             const bool dual = u != v && Tuv.dual;  // (both slots or neither)
-            tri_emit(Tuv, cu, k, &cuv, &luv, lane, dual ? reinterpret_cast<uint16_t*>(Tvu.E.w) : nullptr);
+            tri_emit(Tuv, cu, k, &cuv, &luv, lane, dual ? reinterpret_cast<uint16_t*>(Tvu.E.w) : nullptr,
+                     !Tuv.filt && Tuv.E.mode == BS_REGION);
             if (u != v) {
-              tri_emit(Tvu, cv, (int64_t)pu, &cvu, &lvu, lane, dual ? reinterpret_cast<uint16_t*>(Tuv.E.w) : nullptr);
-              if (cv && vu_win) atomicOr(&s_win[wave][(pu - (uint32_t)p0) >> 5], 1u << (pu & 31u));
+              tri_emit(Tvu, cv, (int64_t)pu, &cvu, &lvu, lane, dual ? reinterpret_cast<uint16_t*>(Tuv.E.w) : nullptr,
+                       !Tvu.filt && Tvu.E.mode == BS_REGION);
+              if (cv && vu_win && !(diag & 2)) atomicOr(&s_win[wave][(pu - (uint32_t)p0) >> 5], 1u << (pu & 31u));
             }
-          } else {
+          } else if (!FILL) {
             const unsigned long long m1 = __ballot(cu), m2 = __ballot(cv);
             cuv += (uint32_t)__popcll(m1);
             cvu += (uint32_t)__popcll(m2);
@@ -538,7 +582,7 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
           tri_epilogue(Tuv, luv, cuv, cvu, lane);
           if (u != v) tri_epilogue(Tvu, lvu, cvu, cuv, lane);
         }
-        if (FILL) {
+        if (FILL && !(diag & 4)) {
           tri_flush(Tuv, nch > 1, lane);
           if (u != v) tri_flush(Tvu, nch > 1, lane);
           if (vu_win) {  // this chunk's window of (v -> u)'s region bits: plain stores, each word once
@@ -1426,6 +1470,8 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
   bs_free(itoff);
   // pass 1: headers
   const unsigned tgrid = std::min<uint32_t>(nitems, 1u << 20);  // <= 2^29 work-items per launch
+  int bs_diag = 0;
+  if (const char* dg = GW_DIAG_ENV("GW_DIAG_BS_FILL")) bs_diag = std::atoi(dg);
   if (nitems) k_bs_tri<false><<<tgrid, kTB>>>(d, items, nitems, d.bs_nbr, nullptr, nullptr, lists_only ? 1 : 0);
   BS_TRY(hipGetLastError());
   // region layout
@@ -1454,7 +1500,7 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
   BS_TRY(hipMemset(d.bs_region, 0, (size_t)words * 4));
   // pass 2: payloads
   if (nitems)
-    k_bs_tri<true><<<tgrid, kTB>>>(d, items, nitems, d.bs_nbr, roff, d.bs_region, lists_only ? 1 : 0);
+    k_bs_tri<true><<<tgrid, kTB>>>(d, items, nitems, d.bs_nbr, roff, d.bs_region, (lists_only ? 1 : 0) | (bs_diag << 8));
   BS_TRY(hipGetLastError());
   BS_TRY(hipDeviceSynchronize());
 #undef BS_TRY

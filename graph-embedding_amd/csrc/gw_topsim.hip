@@ -79,39 +79,40 @@ struct TsArgs {
   unsigned long long* phase;  // diagnostics (GW_DIAG_TS_PHASES): cycles per phase, thread 0 of each block
 };
 
-__device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int* total) {
+template <int NW = TS_WAVES, typename T = int>
+__device__ __forceinline__ T block_excl_scan(T v, T* s_wave, T* total) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int x = v;
+  T x = v;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    int y = __shfl_up(x, o, 64);
+    T y = __shfl_up(x, o, 64);
     if (lane >= o) x += y;
   }
   if (lane == 63) s_wave[wid] = x;
   __syncthreads();
   if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int w = 0; w < TS_WAVES; ++w) {
-      int t = s_wave[w];
+    T acc = 0;
+    for (int w = 0; w < NW; ++w) {
+      T t = s_wave[w];
       s_wave[w] = acc;
       acc += t;
     }
-    s_wave[TS_WAVES] = acc;
+    s_wave[NW] = acc;
   }
   __syncthreads();
-  int r = s_wave[wid] + x - v;
-  *total = s_wave[TS_WAVES];
+  T r = s_wave[wid] + x - v;
+  *total = s_wave[NW];
   __syncthreads();
   return r;
 }
 
-template <typename T>
+template <typename T, int NW = TS_WAVES>
 __device__ __forceinline__ T block_sum(T v, T* s_red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
   if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
   __syncthreads();
   T r = 0;
-  for (int w = 0; w < TS_WAVES; ++w) r += s_red[w];
+  for (int w = 0; w < NW; ++w) r += s_red[w];
   __syncthreads();
   return r;
 }
@@ -186,18 +187,21 @@ struct TsHash {
   __device__ static __forceinline__ uint32_t next(uint32_t h) { return h + 1 == (uint32_t)SLOTS ? 0u : h + 1; }
 };
 
-template <int STEP, int MODE>
+template <int STEP, int MODE, int BLOCK = TS_BLOCK>
 __device__ __forceinline__ void topsim_body(const TsArgs& A) {
+  constexpr int NW = BLOCK / 64;
+  constexpr int CO_LDS = TS_CO_LDS;
   constexpr bool LDS_ROW = MODE == 0;
   using H = TsHash<MODE>;
   constexpr int HASH_SLOTS = H::SLOTS;
   constexpr int HASH_LIMIT = H::LIMIT;
   constexpr int L = 2 * STEP;
   extern __shared__ double s_row[];  // LDS row (LDS_ROW) or hash values+keys
-  __shared__ int s_wave[TS_WAVES + 1];
-  __shared__ long long s_red[TS_WAVES];
+  __shared__ int s_wave[NW + 1];
+  __shared__ long long s_red[NW];
   __shared__ int s_size[L + 2];
-  __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount, s_bin, s_cum, s_exact, s_total;
+  __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount, s_bin, s_cum, s_exact, s_total,
+      s_ncomp, s_all;
   __shared__ unsigned long long s_prefix, s_mask, s_spbase;
   // the output phase's selection arrays share LDS with the levels' child
   // offsets / the walkers' spawner offsets (binary-searched per child / walker)
@@ -206,12 +210,14 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       double sel_val[TOPK_MAX];
       int32_t sel_id[TOPK_MAX];
       unsigned hist[256];
+      unsigned hist2[256];  // radix passes alternate histograms: one is cleared while the other fills
     } out;
-    int32_t co[TS_CO_LDS];
+    int32_t co[CO_LDS];
   } s_u;
   int32_t* const s_sel_id = s_u.out.sel_id;
   double* const s_sel_val = s_u.out.sel_val;
   unsigned* const s_hist = s_u.out.hist;
+  unsigned* const s_hist2 = s_u.out.hist2;
   int32_t* const s_co = s_u.co;
 
   const int tid = threadIdx.x;
@@ -243,9 +249,9 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   long long my_ext = 0, my_upd = 0, my_walk = 0, my_maxf = 0;
 
   if (LDS_ROW) {
-    for (int j = tid; j < n; j += TS_BLOCK) s_row[j] = 0.0;
+    for (int j = tid; j < n; j += BLOCK) s_row[j] = 0.0;
   } else {
-    for (int j = tid; j < HASH_SLOTS; j += TS_BLOCK) {
+    for (int j = tid; j < HASH_SLOTS; j += BLOCK) {
       s_hval[j] = 0.0;
       s_hkey[j] = -1;
     }
@@ -337,6 +343,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     if (tid == 0) {
       s_src = (int)atomicAdd(A.src_counter, 1u);
       s_abort = 0;
+      s_ncomp = 0;
     }
     __syncthreads();
     const int64_t r = s_src;
@@ -372,12 +379,13 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       __syncthreads();
       for (int l = 0; l <= L; ++l) {
         const int sz = s_size[l];
+        if (sz == 0) break;  // every later level is empty too: skip their barriers
         const int32_t* Vl = V + (int64_t)l * cap;
         const double* Ml = M + (int64_t)(l & 1) * cap;
         if (tid == 0 && sz > my_maxf) my_maxf = sz;
         // computePathSim at pathLen = 2i (:80-83, :157) for enumerated nodes
         if ((l & 1) == 0 && l >= 2) {
-          for (int j = tid; j < sz; j += TS_BLOCK) {
+          for (int j = tid; j < sz; j += BLOCK) {
             int32_t path[L + 1], dpath[L + 1];
             int p = j;
 #pragma unroll
@@ -397,10 +405,10 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         }
         if (l == L) break;
         // expansion: child counts (enumerated) and spawners (random branch)
-        int32_t* const COx = sz + 1 <= TS_CO_LDS ? s_co : CO;
+        int32_t* const COx = sz + 1 <= CO_LDS ? s_co : CO;
         int total_children = 0;
         int spawn_base = s_nspawn;
-        for (int base = 0; base < sz; base += TS_BLOCK) {
+        for (int base = 0; base < sz; base += BLOCK) {
           const int j = base + tid;
           int cnt = 0, sp = 0;
           double m = 0.0;
@@ -414,8 +422,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
               sp = 1;  // d == 0: randNeighbor() == -1 -> no child (:143-144)
           }
           int tot_c, tot_s;
-          const int ex_c = block_excl_scan(cnt, s_wave, &tot_c);
-          const int ex_s = block_excl_scan(sp, s_wave, &tot_s);
+          const int ex_c = block_excl_scan<NW>(cnt, s_wave, &tot_c);
+          const int ex_s = block_excl_scan<NW>(sp, s_wave, &tot_s);
           if (j < sz) COx[j] = total_children + ex_c;
           if (sp) {
             const int k = spawn_base + ex_s;
@@ -452,7 +460,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         int32_t* Dn = D + (int64_t)(l + 1) * cap;
         int64_t* On = O + (int64_t)(l + 1) * cap;
         const int64_t* Ol = O + (int64_t)l * cap;
-        for (int c = tid; c < total_children; c += TS_BLOCK) {
+        for (int c = tid; c < total_children; c += BLOCK) {
           const int j = upper_bound_i32(COx, sz + 1, c) - 1;
           const int k = c - COx[j];
           const int d = COx[j + 1] - COx[j];
@@ -472,13 +480,13 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       mark(0);
       // walker index prefix over spawners (queue order)
       const int ns = s_abort ? 0 : s_nspawn;
-      int32_t* const SFx = ns + 1 <= TS_CO_LDS ? s_co : SF;
+      int32_t* const SFx = ns + 1 <= CO_LDS ? s_co : SF;
       int run = 0;
-      for (int base = 0; base < ns; base += TS_BLOCK) {
+      for (int base = 0; base < ns; base += BLOCK) {
         const int k = base + tid;
         const int c = (k < ns) ? SF[k] : 0;
         int tot;
-        const int ex = block_excl_scan(c, s_wave, &tot);
+        const int ex = block_excl_scan<NW>(c, s_wave, &tot);
         if (k < ns) SFx[k] = run + ex;
         run += tot;
       }
@@ -495,8 +503,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     {
       const int W = s_nwalk;
       const int ns = s_nspawn;
-      for (int g = tid; g < W; g += TS_BLOCK) {
-        const int sp = upper_bound_i32(ns + 1 <= TS_CO_LDS ? s_co : SF, ns + 1, g) - 1;
+      for (int g = tid; g < W; g += BLOCK) {
+        const int sp = upper_bound_i32(ns + 1 <= CO_LDS ? s_co : SF, ns + 1, g) - 1;
         const int l0 = SL[sp];
         const double mw = SM[sp];
         int32_t path[L + 1], dpath[L + 1];
@@ -554,7 +562,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     // (a key can straddle the load limit) into the LDS entry
     const int nov = LDS_ROW ? 0 : min((int64_t)s_ntouch, A.touch_cap * 3 / 4);
     if (!LDS_ROW && nov > 0) {
-      for (int k = tid; k < nov; k += TS_BLOCK) {
+      for (int k = tid; k < nov; k += BLOCK) {
         const int32_t slot = touched[k];
         const int32_t key = __hip_atomic_load(&ov_key[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t h = H::slot(key);
@@ -576,24 +584,35 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     // selection passes below scan only them (the others are left empty)
     int NL = 0;
     if (!LDS_ROW) {
-      constexpr int SPT = HASH_SLOTS / TS_BLOCK;
-      static_assert(HASH_SLOTS % TS_BLOCK == 0, "hash slots per thread");
+      constexpr int SPT = HASH_SLOTS / BLOCK;
+      static_assert(HASH_SLOTS % BLOCK == 0, "hash slots per thread");
       int32_t kk[SPT];
       double vv[SPT];
       int mine = 0;
 #pragma unroll
       for (int i = 0; i < SPT; ++i) {
-        kk[i] = s_hkey[tid + i * TS_BLOCK];
-        vv[i] = s_hval[tid + i * TS_BLOCK];
+        kk[i] = s_hkey[tid + i * BLOCK];
+        vv[i] = s_hval[tid + i * BLOCK];
         mine += kk[i] != -1;
       }
-      int tot;
-      int o = block_excl_scan(mine, s_wave, &tot);  // its barriers order every read before the writes
+      // offsets: an inclusive scan inside the wave and one LDS atomic per
+      // wave (the compacted order is free: selection and the sparse-row
+      // writer do not depend on it); the barrier orders every read before the writes
+      const int lane = tid & 63;
+      int incl = mine;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+      }
+      int wbase = 0;
+      if (lane == 63) wbase = atomicAdd(&s_ncomp, incl);
+      int o = __shfl(wbase, 63, 64) + incl - mine;
 #pragma unroll
       for (int i = 0; i < SPT; ++i)
         if (kk[i] != -1) {
-          s_hkey[tid + i * TS_BLOCK] = -1;
-          s_hval[tid + i * TS_BLOCK] = 0.0;
+          s_hkey[tid + i * BLOCK] = -1;
+          s_hval[tid + i * BLOCK] = 0.0;
         }
       __syncthreads();
 #pragma unroll
@@ -604,7 +623,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           ++o;
         }
       __syncthreads();
-      NL = tot;
+      NL = s_ncomp;
     }
     const int NC = LDS_ROW ? n : NL + nov;
     auto cand = [&](int idx, int32_t* id, double* val) -> bool {
@@ -624,11 +643,11 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     if (A.out_rows) {
       double* orow = A.out_rows + r * (int64_t)n;
       if (LDS_ROW) {
-        for (int t = tid; t < n; t += TS_BLOCK) orow[t] = s_row[t];
+        for (int t = tid; t < n; t += BLOCK) orow[t] = s_row[t];
       } else {
-        for (int t = tid; t < n; t += TS_BLOCK) orow[t] = 0.0;
+        for (int t = tid; t < n; t += BLOCK) orow[t] = 0.0;
         __syncthreads();
-        for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+        for (int idx = tid; idx < NC; idx += BLOCK) {
           int32_t id;
           double v;
           if (cand(idx, &id, &v)) orow[id] = v;
@@ -640,20 +659,20 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       // claimed offset; a row that does not fit is skipped (len -1) but still
       // counted, so the cursor ends at the room all rows need
       int mine = 0;
-      for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+      for (int idx = tid; idx < NC; idx += BLOCK) {
         int32_t id;
         double v;
         mine += cand(idx, &id, &v) ? 1 : 0;
       }
       int tot;
-      const int ex = block_excl_scan(mine, s_wave, &tot);
+      const int ex = block_excl_scan<NW>(mine, s_wave, &tot);
       if (tid == 0) s_spbase = atomicAdd(A.sp.cursor, (unsigned long long)tot);
       __syncthreads();
       const int64_t base = (int64_t)s_spbase;
       const bool fits = base + tot <= A.sp.cap;
       if (fits) {
         int64_t o = base + ex;
-        for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+        for (int idx = tid; idx < NC; idx += BLOCK) {
           int32_t id;
           double v;
           if (cand(idx, &id, &v)) {
@@ -674,7 +693,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       // the K-th key's bin may be taken whole once everything at or above it
       // fits the selection arrays: the ordering pass below then ranks the
       // extra entries out (bounded so that it keeps 4 threads per entry)
-      const int kcoll = max(K, TS_BLOCK / 4);
+      const int kcoll = max(K, BLOCK / 4);
       mark(5);
       unsigned long long T = 0;  // threshold key (K-th largest)
       int32_t idT = 0x7fffffff;  // largest id taken at key == T
@@ -682,41 +701,52 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       bool bin_exact = false;    // the K-th key's bin is taken whole: select by masked prefix
       unsigned long long Tmask = ~0ull;
       {
+        for (int b = tid; b < 256; b += BLOCK) s_hist[b] = 0;
         if (tid == 0) {
           s_prefix = 0;
           s_mask = 0;
           s_need = K;
           s_exact = 0;
           s_total = 0;
+          s_all = 0;
         }
         __syncthreads();
-        for (int shift = 56; shift >= 0; shift -= 8) {
-          for (int b = tid; b < 256; b += TS_BLOCK) s_hist[b] = 0;
-          __syncthreads();
+        // two barriers a pass: the histogram (the next pass's one is cleared
+        // meanwhile), then wave 0 picks the bin and narrows the prefix
+        int pass = 0;
+        for (int shift = 56; shift >= 0; shift -= 8, ++pass) {
+          unsigned* const H = (pass & 1) ? s_hist2 : s_hist;
+          unsigned* const Hn = (pass & 1) ? s_hist : s_hist2;
           const unsigned long long pre = s_prefix, msk = s_mask;
-          for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+          for (int b = tid; b < 256; b += BLOCK) Hn[b] = 0;
+          for (int idx = tid; idx < NC; idx += BLOCK) {
             int32_t id;
             double v;
             if (!cand(idx, &id, &v)) continue;
             const unsigned long long k = dkey(v);
-            if ((k & msk) == pre) atomicAdd(&s_hist[(k >> shift) & 255], 1u);
+            if ((k & msk) == pre) atomicAdd(&H[(k >> shift) & 255], 1u);
           }
           __syncthreads();
-          if (tid < 64) select_bin(s_hist, s_need, true, &s_bin, &s_cum, shift == 56 ? &s_total : nullptr);
+          if (tid < 64) {
+            select_bin(H, s_need, true, &s_bin, &s_cum, shift == 56 ? &s_total : nullptr);
+            if (tid == 0) {  // s_bin / s_cum / s_total were written by this thread
+              if (shift == 56 && s_total <= K) {
+                s_all = 1;
+              } else {
+                const int rest = s_need - s_cum;
+                // everything above the chosen bin (K - rest keys) plus the bin fits
+                if (K - rest + (int)H[s_bin] <= kcoll) s_exact = 1;
+                s_need = rest;
+                s_prefix = pre | ((unsigned long long)s_bin << shift);
+                s_mask = msk | (255ull << shift);
+              }
+            }
+          }
           __syncthreads();
-          if (shift == 56 && s_total <= K) {
+          if (s_all) {
             take_all = true;
             break;
           }
-          if (tid == 0) {
-            const int rest = s_need - s_cum;
-            // everything above the chosen bin (K - rest keys) plus the bin fits
-            if (K - rest + (int)s_hist[s_bin] <= kcoll) s_exact = 1;
-            s_need = rest;
-            s_prefix = pre | ((unsigned long long)s_bin << shift);
-            s_mask = msk | (255ull << shift);
-          }
-          __syncthreads();
           if (s_exact) break;
         }
         bin_exact = s_exact != 0;
@@ -727,12 +757,12 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       if (!take_all && !bin_exact) {
         // ties at the threshold: smallest ids first
         long long eq_local = 0;
-        for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+        for (int idx = tid; idx < NC; idx += BLOCK) {
           int32_t id;
           double v;
           if (cand(idx, &id, &v) && dkey(v) == T) ++eq_local;
         }
-        const int EQ = (int)block_sum<long long>(eq_local, s_red);
+        const int EQ = (int)block_sum<long long, NW>(eq_local, s_red);
         if (EQ > s_need) {
           if (tid == 0) {
             s_prefix = 0;
@@ -740,10 +770,10 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           }
           __syncthreads();
           for (int shift = 24; shift >= 0; shift -= 8) {
-            for (int b = tid; b < 256; b += TS_BLOCK) s_hist[b] = 0;
+            for (int b = tid; b < 256; b += BLOCK) s_hist[b] = 0;
             __syncthreads();
             const unsigned long long pre = s_prefix, msk = s_mask;
-            for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+            for (int idx = tid; idx < NC; idx += BLOCK) {
               int32_t id;
               double v;
               if (!cand(idx, &id, &v) || dkey(v) != T) continue;
@@ -766,7 +796,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       mark(7);
       if (tid == 0) s_cnt = 0;
       __syncthreads();
-      for (int idx = tid; idx < NC; idx += TS_BLOCK) {
+      for (int idx = tid; idx < NC; idx += BLOCK) {
         int32_t id;
         double v;
         if (!cand(idx, &id, &v)) continue;
@@ -787,28 +817,31 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       int32_t* oid = A.out_ids + r * (int64_t)K;
       double* osc = A.out_scores + r * (int64_t)K;
       {
-        // G threads per entry (cnt <= 128: 4, else 2), partial counts summed with lane shuffles
-        const int G = cnt <= TS_BLOCK / 4 ? 4 : 2;
-        const int i = tid / G, sub = tid % G;
-        int rank = 0;
-        double vi = 0.0;
-        int32_t ii = 0;
-        if (i < cnt) {
-          vi = s_sel_val[i];
-          ii = s_sel_id[i];
+        // G threads per entry (4 while cnt <= BLOCK / 4, then 2, then 1; more
+        // entries than threads take several passes), partial counts summed with lane shuffles
+        const int G = cnt <= BLOCK / 4 ? 4 : cnt <= BLOCK / 2 ? 2 : 1;
+        for (int i0 = 0; i0 < cnt; i0 += BLOCK / G) {
+          const int i = i0 + tid / G, sub = tid % G;
+          int rank = 0;
+          double vi = 0.0;
+          int32_t ii = 0;
+          if (i < cnt) {
+            vi = s_sel_val[i];
+            ii = s_sel_id[i];
 #pragma unroll 4
-          for (int j = sub; j < cnt; j += G) {
-            const double vj = s_sel_val[j];
-            rank += (vj > vi) || (vj == vi && s_sel_id[j] < ii);
+            for (int j = sub; j < cnt; j += G) {
+              const double vj = s_sel_val[j];
+              rank += (vj > vi) || (vj == vi && s_sel_id[j] < ii);
+            }
+          }
+          for (int o = 1; o < G; o <<= 1) rank += __shfl_xor(rank, o, 64);
+          if (i < cnt && sub == 0 && rank < K) {
+            oid[rank] = ii;
+            osc[rank] = vi;
           }
         }
-        for (int o = 1; o < G; o <<= 1) rank += __shfl_xor(rank, o, 64);
-        if (i < cnt && sub == 0 && rank < K) {
-          oid[rank] = ii;
-          osc[rank] = vi;
-        }
       }
-      for (int k = min(cnt, K) + tid; k < K; k += TS_BLOCK) {
+      for (int k = min(cnt, K) + tid; k < K; k += BLOCK) {
         oid[k] = -1;
         osc[k] = 0.0;
       }
@@ -817,13 +850,13 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     mark(9);
     // re-zero the accumulator for the next source
     if (LDS_ROW) {
-      for (int t = tid; t < n; t += TS_BLOCK) s_row[t] = 0.0;
+      for (int t = tid; t < n; t += BLOCK) s_row[t] = 0.0;
     } else {
-      for (int j = tid; j < NL; j += TS_BLOCK) {  // occupied slots were compacted to [0, NL)
+      for (int j = tid; j < NL; j += BLOCK) {  // occupied slots were compacted to [0, NL)
         s_hval[j] = 0.0;
         s_hkey[j] = -1;
       }
-      for (int k = tid; k < nov; k += TS_BLOCK) {
+      for (int k = tid; k < nov; k += BLOCK) {
         const int32_t slot = touched[k];
         __hip_atomic_store(&ov_key[slot], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&ov_val[slot], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -841,9 +874,9 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   if (kGwDiag && A.phase && tid == 0)
     for (int k = 0; k < 10; ++k) atomicAdd(&A.phase[k], s_ph[k]);
   // statistics
-  long long e = block_sum<long long>(my_ext, s_red);
-  long long u = block_sum<long long>(my_upd, s_red);
-  long long w = block_sum<long long>(my_walk, s_red);
+  long long e = block_sum<long long, NW>(my_ext, s_red);
+  long long u = block_sum<long long, NW>(my_upd, s_red);
+  long long w = block_sum<long long, NW>(my_walk, s_red);
   if (tid == 0 && A.stats) {
     atomicAdd((unsigned long long*)&A.stats[0], (unsigned long long)e);
     atomicAdd((unsigned long long*)&A.stats[1], (unsigned long long)u);
