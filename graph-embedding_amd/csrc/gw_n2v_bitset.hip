@@ -48,6 +48,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "gw_device_common.h"
 
@@ -297,10 +298,12 @@ constexpr int kTW = kTB / 64;
 constexpr int kTriH = 4096;                  // ids of N(u) per hash chunk
 constexpr int kTriS = 2 * kTriH;             // LDS hash slots (load factor <= 1/2)
 constexpr int kTriEB = 512;                  // edges of u's row per work item
+constexpr int kTriAhead = 4;                 // rounds of N(v) in flight per wave
+constexpr int32_t kTriNotOwned = INT32_MIN;
 
 // build-time model constants (gw_bitset_build_model_s), measured on MI355X
-// (R-MAT-20: 0.19 s for sum(min deg) = 6.9e9; R-MAT-24 ef 6: 1.28 s for 4.4e10)
-constexpr double kBuildProbeRate = 6.9e10;     // k_bs_tri stream probes per second (one pass)
+// (R-MAT-20: 0.175 s for sum(min deg) = 6.9e9; R-MAT-24 ef 6: 1.17 s for 4.4e10)
+constexpr double kBuildProbeRate = 7.7e10;     // k_bs_tri stream probes per second (one pass)
 constexpr double kBuildSlotSeconds = 5.0e-11;  // per adjacency slot: memset, headers, sizes scan, payload stores
 
 struct TriItem {
@@ -440,6 +443,7 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
   // per-edge state between chunks (hubs): common counts, last positions, kp(u -> v), cursor in N(v)
   __shared__ uint32_t s_cuv[kTriEB], s_cvu[kTriEB], s_cur[kTriEB];
   __shared__ int32_t s_luv[kTriEB], s_lvu[kTriEB], s_kp[kTriEB];
+  __shared__ int32_t s_nx[kTriEB];  // hubs: N(v)'s next element (kTriNotOwned: edge owned by v)
   __shared__ uint32_t s_stage[kTW][2][12];  // pass 2: both slots' payload words, per wave
   // pass 2: the (v -> u) slot's region bits of this chunk (positions p0 ..
   // p0 + kTriH of N(u): one aligned window per chunk, written once)
@@ -480,10 +484,19 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
       // of N(v) falls in exactly one chunk's stream
       const int32_t hi = ch == nch - 1 ? INT32_MAX : G.nbrs[ub + p1 - 1];
       for (int64_t j = j0 + wave; j < j1; j += kTW) {
+        const int li = (int)(j - j0);
+        if (ch > 0) {
+          // hubs: an edge whose next element of N(v) lies past this chunk's
+          // range has nothing here (the last chunk still closes every owned edge)
+          const int32_t nx = s_nx[li];
+          if (nx == kTriNotOwned || (ch + 1 < nch && nx > hi)) continue;
+        }
         const int32_t v = G.nbrs[ub + j];
         const int64_t vb = G.offsets[v], dv = G.offsets[v + 1] - vb;
-        if (!(du > dv || (du == dv && u <= v))) continue;  // the other end owns this edge
-        const int li = (int)(j - j0);
+        if (!(du > dv || (du == dv && u <= v))) {  // the other end owns this edge
+          if (nch > 1 && lane == 0) s_nx[li] = kTriNotOwned;
+          continue;
+        }
         const int64_t e = ub + j;
         uint32_t cuv = 0, cvu = 0, cur = 0;
         int64_t luv = -1, lvu = -1, kp = -1;
@@ -495,10 +508,14 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
           lvu = s_lvu[li];
           kp = s_kp[li];
         }
-        // the first round's elements are requested before pass 2's header
-        // reads, so the two latencies overlap
+        // the stream keeps kTriAhead rounds of N(v) in flight per wave (the
+        // probes are latency-bound otherwise); the first ones are requested
+        // before pass 2's header reads, so those latencies overlap too
         int64_t k = (int64_t)cur + lane;
         int32_t x = k < dv ? G.nbrs[vb + k] : INT32_MAX;
+        int32_t xa[kTriAhead - 1];
+#pragma unroll
+        for (int r = 0; r < kTriAhead - 1; ++r) xa[r] = k + 64 * (r + 1) < dv ? G.nbrs[vb + k + 64 * (r + 1)] : INT32_MAX;
         // pass 2: both slots' payload writers (headers from pass 1)
         TriSlot Tuv, Tvu;
         int64_t er = -1;
@@ -520,12 +537,12 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
             Tvu.E.nobits = vu_win;  // region bits go through the LDS window
           }
         }
+        int32_t nx = INT32_MAX;  // first element of N(v) past this chunk (INT32_MAX: row done)
         for (;;) {
-          // the next round's elements are requested before this round is
-          // probed, so a wave keeps one row read in flight while it works (the
-          // extra read past the row's or the chunk's end costs one line)
-          const int64_t kn = k + 64;
-          const int32_t xn = kn < dv ? G.nbrs[vb + kn] : INT32_MAX;
+          // the round kTriAhead ahead is requested before this one is probed
+          // (reads past the chunk's end cost a line each, past the row's end nothing)
+          const int64_t kf = k + 64 * kTriAhead;
+          const int32_t xf = kf < dv ? G.nbrs[vb + kf] : INT32_MAX;
           const bool inr = k < dv && x <= hi;
           bool hit = false;
           uint32_t pu = 0;
@@ -574,9 +591,15 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
           }
           const int nin = __popcll(__ballot(inr));  // a prefix of the lanes (rows are sorted)
           cur += (uint32_t)nin;
-          if (nin < 64) break;  // the chunk's id range or the row ended
-          k = kn;
-          x = xn;
+          if (nin < 64) {  // the chunk's id range or the row ended
+            nx = __shfl(x, nin, 64);
+            break;
+          }
+          k += 64;
+          x = xa[0];
+#pragma unroll
+          for (int r = 0; r < kTriAhead - 2; ++r) xa[r] = xa[r + 1];
+          xa[kTriAhead - 2] = xf;
         }
         if (FILL && ch + 1 == nch) {
           tri_epilogue(Tuv, luv, cuv, cvu, lane);
@@ -605,6 +628,7 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
             s_luv[li] = (int32_t)luv;
             s_lvu[li] = (int32_t)lvu;
             s_kp[li] = (int32_t)kp;
+            s_nx[li] = nx;
           }
           continue;
         }
@@ -1454,12 +1478,23 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
   int32_t* dkey = nullptr;  // sorted degrees (discarded)
   if ((rc = bs_alloc(g, &dkey, n))) return fail(rc);
   BS_TRY(hipcub::DeviceRadixSort::SortPairsDescending(tmp, tb, d.deg, dkey, ids, order, (int)n));
+  // diagnostics build (GW_DIAG_BS_FILL & 8): both passes launched as two
+  // dispatches, vertices of degree > 64 and the rest, to time them apart
+  int bs_diag = 0;
+  if (const char* dg = GW_DIAG_ENV("GW_DIAG_BS_FILL")) bs_diag = std::atoi(dg);
+  int64_t nbig = 0;
+  if (bs_diag & 8) {
+    std::vector<int32_t> hk((size_t)n);
+    BS_TRY(hipMemcpy(hk.data(), dkey, (size_t)n * 4, hipMemcpyDeviceToHost));
+    while (nbig < n && hk[(size_t)nbig] > 64) ++nbig;
+  }
   bs_free(dkey);
   k_bs_nitems<<<gn1, kB>>>(d, order, nit);
   BS_TRY(hipGetLastError());
   BS_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, nit, itoff, (int)(n + 1)));
-  uint32_t nitems = 0;
+  uint32_t nitems = 0, isplit = 0;
   BS_TRY(hipMemcpy(&nitems, itoff + n, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (bs_diag & 8) BS_TRY(hipMemcpy(&isplit, itoff + nbig, sizeof(uint32_t), hipMemcpyDeviceToHost));
   if ((rc = bs_alloc(g, &items, std::max<int64_t>(nitems, 1)))) return fail(rc);
   k_bs_items<<<gn, kB>>>(d, order, itoff, items);
   BS_TRY(hipGetLastError());
@@ -1469,10 +1504,23 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
   bs_free(nit);
   bs_free(itoff);
   // pass 1: headers
-  const unsigned tgrid = std::min<uint32_t>(nitems, 1u << 20);  // <= 2^29 work-items per launch
-  int bs_diag = 0;
-  if (const char* dg = GW_DIAG_ENV("GW_DIAG_BS_FILL")) bs_diag = std::atoi(dg);
-  if (nitems) k_bs_tri<false><<<tgrid, kTB>>>(d, items, nitems, d.bs_nbr, nullptr, nullptr, lists_only ? 1 : 0);
+  auto tri = [&](bool fill, const TriItem* it, uint32_t cnt) {
+    if (!cnt) return;
+    const unsigned tgrid = std::min<uint32_t>(cnt, 1u << 20);  // <= 2^29 work-items per launch
+    if (fill)
+      k_bs_tri<true><<<tgrid, kTB>>>(d, it, cnt, d.bs_nbr, roff, d.bs_region, (lists_only ? 1 : 0) | (bs_diag << 8));
+    else
+      k_bs_tri<false><<<tgrid, kTB>>>(d, it, cnt, d.bs_nbr, nullptr, nullptr, lists_only ? 1 : 0);
+  };
+  auto tri_all = [&](bool fill) {
+    if (bs_diag & 8) {
+      tri(fill, items, isplit);
+      tri(fill, items + isplit, nitems - isplit);
+    } else {
+      tri(fill, items, nitems);
+    }
+  };
+  tri_all(false);
   BS_TRY(hipGetLastError());
   // region layout
   if ((rc = bs_alloc(g, &sz, nnz + 1)) || (rc = bs_alloc(g, &roff, nnz + 1))) return fail(rc);
@@ -1499,8 +1547,7 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
   if ((rc = bs_alloc(g, &d.bs_region, (int64_t)words))) return fail(rc);
   BS_TRY(hipMemset(d.bs_region, 0, (size_t)words * 4));
   // pass 2: payloads
-  if (nitems)
-    k_bs_tri<true><<<tgrid, kTB>>>(d, items, nitems, d.bs_nbr, roff, d.bs_region, (lists_only ? 1 : 0) | (bs_diag << 8));
+  tri_all(true);
   BS_TRY(hipGetLastError());
   BS_TRY(hipDeviceSynchronize());
 #undef BS_TRY
