@@ -328,6 +328,68 @@ def _hub_edgelist(path):
             f.write(f"{a} {b}\n")
 
 
+def _multichunk_hub_edgelist(path):
+    """Hub 0 of degree 13,999 (four 4,096-id hash chunks in the build) and a
+    second hub 1 adjacent to ids 2..7000, so slot (0 -> 1) / (1 -> 0) has
+    ~7,000 common neighbours spread over two of hub 0's chunks (region bits of
+    the (v -> u) slot from several chunk windows, payloads OR-merged across
+    chunks).  Every other vertex links to 8 ids within +-300 of itself, so the
+    stream of N(v) for an edge (0, v) has nothing in most of hub 0's chunks:
+    the build skips those (per-edge next element), which only happens for
+    hubs with three or more chunks."""
+    rng = np.random.default_rng(99)
+    n = 14000
+    E = {(0, v) for v in range(1, n)}
+    E |= {(1, v) for v in range(2, 7001)}
+    for u in range(2, n):
+        lo, hi = max(2, u - 300), min(n - 1, u + 300)
+        for v in rng.integers(lo, hi + 1, 8):
+            if int(v) != u:
+                E.add((min(u, int(v)), max(u, int(v))))
+    with open(path, "w") as f:
+        for a, b in sorted(E):
+            f.write(f"{a} {b}\n")
+
+
+@pytest.mark.parametrize("mode", ["bitset", "rejection"])
+@pytest.mark.parametrize("p,q", [(0.25, 4), (4, 0.25)])
+def test_multichunk_hub_builds_equal_oracle(gw, oracle, tmp_path, mode, p, q):
+    """Walks over tables built for hubs spanning 4 hash chunks (chunk skips,
+    cross-chunk merges) equal the oracle: bitset tables and the listed
+    rejection sampler's lists-only build."""
+    import torch
+    from gwamd import _lib as C
+    path = str(tmp_path / "mchub.edgelist")
+    _multichunk_hub_edgelist(path)
+    G = gw.GWGraph.from_edgelist(path, " ", "nx").to_device(0)
+    if mode == "rejection":
+        G.options(listed=1)
+    C.check(C.lib().gw_n2v_prepare(G.handle, float(p), float(q),
+                                   C.N2V_BITSET if mode == "bitset" else C.N2V_REJECTION), G.handle)
+    inf = G.info()
+    assert inf.max_degree > 3 * 4096
+    if mode == "rejection":
+        assert inf.listed == 1
+    L, begin, count = 30, 123, 6000
+    out = torch.empty((count, L), dtype=torch.int32, device="cuda")
+    lens = torch.empty(count, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    C.check(C.lib().gw_n2v_walks(G.handle, L, 5, begin, count, 1, C.ptr(out), C.ptr(lens), C.ptr(cnt), None),
+            G.handle)
+    torch.cuda.synchronize()
+    csr = G.export_csr()
+    if mode == "bitset":
+        ref, rl, rc = oracle.walks_bitset(csr, p, q, 5, L, begin, count, nthreads=8)
+    else:
+        ref, rl, rc = oracle.walks_scale(dict(csr, weights=None), p, q, 5, L, begin, count, nthreads=8)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    np.testing.assert_array_equal(lens.cpu().numpy(), rl)
+    assert int(cnt[0]) == int(rc[0]) and int(cnt[1]) == int(rc[1])
+    o = out.cpu().numpy()
+    assert (o == 0).sum() > count // 2 and (o == 1).sum() > 0  # the walks do pass through both hubs
+    G.free()
+
+
 @pytest.mark.parametrize("p,q", [(0.25, 4), (4, 0.25)])
 def test_bitset_directory_hub_equals_oracle(gw, oracle, tmp_path, p, q):
     import torch
