@@ -434,7 +434,7 @@ __device__ __forceinline__ void tri_emit(const F& f, bool on, int64_t pos, uint3
 // (a launch's work-items must stay below 2^32, so a workgroup takes items
 // blockIdx.x, blockIdx.x + gridDim.x, ...; hubs come first in the item order)
 template <bool FILL>
-__global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* __restrict__ items, uint32_t nitems,
+__global__ void __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) k_bs_tri(gw_dev_graph G, const TriItem* __restrict__ items, uint32_t nitems,
                                                 gw_bs_nbr* __restrict__ bsn,
                                                 const uint64_t* __restrict__ roff, uint32_t* __restrict__ reg,
                                                 int lists_only) {
@@ -483,7 +483,28 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
       // this chunk's id range is (previous chunk's last id, hi]: every element
       // of N(v) falls in exactly one chunk's stream
       const int32_t hi = ch == nch - 1 ? INT32_MAX : G.nbrs[ub + p1 - 1];
-      for (int64_t j = j0 + wave; j < j1; j += kTW) {
+      // the wave's edges are software-pipelined: the row bounds of its next
+      // edge and the neighbour id of the one after are requested at the top of
+      // each edge, so an edge starts with (v, row) in registers instead of a
+      // chain of two dependent reads
+      int64_t jp = j0 + wave;
+      int32_t pv_n = jp + kTW < j1 ? G.nbrs[ub + jp + kTW] : 0;
+      int32_t pv = 0;
+      int64_t pvb = 0, pve = 0;
+      if (jp < j1) {
+        pv = G.nbrs[ub + jp];
+        pvb = G.offsets[pv];
+        pve = G.offsets[pv + 1];
+      }
+      for (int64_t j = jp; j < j1; j += kTW) {
+        const int32_t v = pv;
+        const int64_t vb = pvb, dv = pve - pvb;
+        if (j + kTW < j1) {
+          pv = pv_n;
+          pvb = G.offsets[pv];
+          pve = G.offsets[pv + 1];
+        }
+        if (j + 2 * kTW < j1) pv_n = G.nbrs[ub + j + 2 * kTW];
         const int li = (int)(j - j0);
         if (ch > 0) {
           // hubs: an edge whose next element of N(v) lies past this chunk's
@@ -491,8 +512,6 @@ __global__ void __launch_bounds__(kTB) k_bs_tri(gw_dev_graph G, const TriItem* _
           const int32_t nx = s_nx[li];
           if (nx == kTriNotOwned || (ch + 1 < nch && nx > hi)) continue;
         }
-        const int32_t v = G.nbrs[ub + j];
-        const int64_t vb = G.offsets[v], dv = G.offsets[v + 1] - vb;
         if (!(du > dv || (du == dv && u <= v))) {  // the other end owns this edge
           if (nch > 1 && lane == 0) s_nx[li] = kTriNotOwned;
           continue;

@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests/test_n2v_gpu.py -x -q --timeout 300 --timeout-method thread -k "bitset or auto or directory" > gpurun_out/t_r03k.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_n2v_gpu.py -x -q --timeout 300 --timeout-method thread -k "bitset or auto or directory or multichunk" > gpurun_out/t_r03k.log 2>&1
 rc=$?; echo TEST_RC=$rc; tail -3 gpurun_out/t_r03k.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_build_k -o bt -- python tools/build_time.py --graphs r20,r24e6 --modes bitset --reps 2 > gpurun_out/build_time_k.json 2> gpurun_out/build_time_k.err
