@@ -46,7 +46,8 @@ constexpr int64_t LDS_ROW_MAX_BYTES = 96 * 1024;
 struct TsArgs {
   gw_dev_graph G;
   int variant;
-  int diag;  // GW_DIAG_TS (timing experiments only, wrong results): 1 = walkers skip computePathSim, 2 = cheap RNG
+  int diag;  // GW_DIAG_TS (timing experiments only, wrong results): 1 = walkers skip computePathSim, 2 = cheap RNG,
+             // 4 / 8 = walker reads confined to the first 2^26 / 2^27 slot entries
   int sample;
   double sampled;
   double cache[16];
@@ -541,7 +542,10 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
                 ux = u.x;
                 uy = u.y;
               }
-              const gw_ts_ent e = gw_ts_load(A.ent + ocur + gw_index(ux, uy, (uint32_t)dcur));  // randNeighbor
+              uint64_t ei = (uint64_t)ocur + gw_index(ux, uy, (uint32_t)dcur);
+              if (kGwDiag && (A.diag & 12))  // timing only: walker reads confined to 1 GB / 2 GB of the table
+                ei &= (A.diag & 4) ? ((1ull << 26) - 1) : ((1ull << 27) - 1);
+              const gw_ts_ent e = gw_ts_load(A.ent + ei);  // randNeighbor
               path[t] = e.x;
               dpath[t] = e.d;
               dcur = e.d;

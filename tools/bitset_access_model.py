@@ -79,6 +79,9 @@ def main():
     ap.add_argument("--tail-list", type=int, default=0,
                     help="what-if: entries with c <= this also carry their commons as positions in N(u)")
     ap.add_argument("--pdir", type=int, default=8, help="directory blocks kept in the entry (0: none)")
+    ap.add_argument("--hub-bits", type=int, default=0,
+                    help="what-if: every entry (u -> x) whose payload has room carries a bitmap of x's "
+                         "adjacency to the H highest-degree vertices, answering membership of a hub prev")
     a = ap.parse_args()
     import gwamd
     import oracle
@@ -86,6 +89,9 @@ def main():
     csr = G.export_csr()
     off, nbrs = csr["offsets"], csr["nbrs"]
     n = len(off) - 1
+    deg = np.diff(off)
+    hub_rank = np.full(n, n, dtype=np.int64)
+    hub_rank[np.argsort(-deg, kind="stable")] = np.arange(n)
     L = 80
     begin = 7 * n + 11  # a window inside the bench's first step
     W, lens, _ = oracle.walks_bitset(csr, a.p, a.q, a.seed, L, begin, a.walks, nthreads=8)
@@ -160,6 +166,16 @@ def main():
                         cx = int(np.isin(rx, row, assume_unique=True).sum()) - int(cur in set(rx.tolist()))
                         if cx <= a.tail_list and d < 65536:
                             add("membership_word_answered_by_candidate_tail_list")
+                    if a.hub_bits:
+                        if hub_rank[prev] < a.hub_bits:
+                            add(f"membership_word_prev_in_top{a.hub_bits}")
+                            x = int(row[k])
+                            rx = nbrs[off[x]:off[x + 1]]
+                            cx = int(np.isin(rx, row, assume_unique=True).sum()) - int(cur in set(rx.tolist()))
+                            # room: a list of cx u16 beside the bitmap, or the other modes' payload bits
+                            room = (16 * cx + a.hub_bits <= a.payload_bits) if cx <= a.list_max else False
+                            if room and len(rx) < 65536:
+                                add("membership_word_answered_by_candidate_hub_bitmap")
                 if k != kp and k not in cset:
                     break
                 add("other_retries")

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--modes", default="2,3")
     ap.add_argument("--graphs", default="p10m,arxiv")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--env", default="GW_DIAG_TS_HASH", help="diag knob the modes are values of")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -64,7 +65,7 @@ def main():
         sh = C.ctypes.c_void_p(stream.cuda_stream)
         for rep in range(a.reps):
             for m in modes:
-                os.environ["GW_DIAG_TS_HASH"] = m
+                os.environ[a.env] = m
                 C.check(C.lib().gw_topsim_prepare(h, C.TOPSIM_SINGLE_SAMPLE, sample, step, K), h)
                 r = res[m]
                 for timed in (False, True):
