@@ -163,6 +163,7 @@ struct gw_graph {
   uint32_t* sr_ent = nullptr;    // [nnz + pad] byte offset of the compact neighbour
   uint16_t* sr_heads = nullptr;  // [(nnz + pad) / 16] head-of-row bits
   int64_t* sr_off = nullptr;   // [m+1] compact offsets
+  int64_t* sr_poff = nullptr;  // [m+1] offsets of the row-padded stream (rows start on 16-entry chunks)
   int32_t* sr_rows = nullptr;  // [m] compact id -> vertex
   int64_t sr_n = 0, sr_m = 0;
   std::string err;

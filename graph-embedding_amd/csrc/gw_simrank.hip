@@ -17,11 +17,13 @@
 //                                     for j > i, written to [i][j] and [j][i]
 // Both passes run on the compact graph of non-isolated vertices (m <= n);
 // each workgroup owns one row i: the row is staged in LDS (when m*8 fits),
-// the adjacency is streamed as a flat, head-flagged entry list (4 B/entry,
-// 16 B per lane, prefetched one chunk ahead), and the per-row sums are
-// lane-local sums + a DPP segmented scan per 256 entries, with the row's
-// carry kept in registers.  Work per pass = n * nnz
-// gathered doubles (pass 2 about half of it).  The reduction order differs
+// the adjacency is streamed as a row-padded entry list (4 B/entry, every row
+// starts on a 16-entry chunk, padding reads a zero slot; 16 entries = 64 B
+// per lane, prefetched one chunk ahead), so a lane's 16 entries belong to
+// ONE row: the per-row sums are a plain 16-term lane sum + a DPP segmented
+// scan over the wave's 64 chunk partials, with the row's carry kept in
+// registers.  Work per pass = n * nnz gathered doubles (pass 2 about half of
+// it) plus the padding (blog: +12.6%).  The reduction order differs
 // from the Java double loop (fp64 reassociation only, ~1e-16 relative);
 // each S'[i][j] is computed once and mirrored, so S stays exactly symmetric.
 #include <hip/hip_runtime.h>
@@ -47,9 +49,10 @@ constexpr int64_t SR_MIN_WIN = 2048;             // smallest output window (rows
 // segment length — no per-row lookups inside the loop.
 struct SrArgs {
   int64_t m;
-  const int64_t* off;   // [m+1] compact CSR offsets
-  const uint32_t* ent;    // [nnz + pad] byte offset (8 * compact neighbour) into a row
-  const uint16_t* heads;  // [(nnz + pad) / 16] bit k of word g: entry 16g+k starts a row
+  const int64_t* off;     // [m+1] compact CSR offsets (degrees)
+  const int64_t* poff;    // [m+1] row starts in the padded stream (multiples of SR_K)
+  const uint32_t* ent;    // [poff[m] + SR_CHUNK] byte offset (8 * compact neighbour) into a row; padding 8 * m
+  const uint16_t* heads;  // [(poff[m] + SR_CHUNK) / 16] bit 0 of word g: chunk g (entries 16g..16g+15) starts a row
   double C;
 };
 
@@ -140,32 +143,35 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_gather(SrArgs A, const double* 
   extern __shared__ double lds[];
   const int64_t m = A.m;
   double* const in_row = lds;
-  double* const out_win = LDS_ROW ? lds + m : lds;
+  double* const out_win = LDS_ROW ? lds + m + 1 : lds;
   const int64_t i = blockIdx.x;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int32_t di = (int32_t)(A.off[i + 1] - A.off[i]);
   if (PASS2 && threadIdx.x == 0) dst[i * m + i] = last ? 0.0 : 1.0;  // tempSim[i][i] stays 1
   const double* row = src + i * m;
-  if (LDS_ROW)
+  if (LDS_ROW) {
     for (int64_t b = threadIdx.x; b < m; b += SR_BLOCK) in_row[b] = row[b];
+    if (threadIdx.x == 0) in_row[m] = 0.0;  // the padding entries' slot
+  }
+  const uint32_t pad_off = (uint32_t)m * 8u;
   const uint64_t below_incl = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
 
   for (int64_t j0 = PASS2 ? i + 1 : 0; j0 < m; j0 += win) {
     const int64_t j1 = min(m, j0 + (int64_t)win);
     __syncthreads();  // in_row staged / previous window flushed
     {
-      const int64_t e_lo = A.off[j0], tot = A.off[j1] - e_lo;
+      const int64_t e_lo = A.poff[j0], tot = A.poff[j1] - e_lo;
       const int64_t t0 = e_lo + tot * wave / SR_WAVES, t1 = e_lo + tot * (wave + 1) / SR_WAVES;
-      const int64_t ra = wave == 0 ? j0 : first_row_at(A.off, j0, j1, t0);
-      const int64_t rb = wave == SR_WAVES - 1 ? j1 : first_row_at(A.off, j0, j1, t1);
-      const int64_t eb = A.off[ra], ee = A.off[rb];
+      const int64_t ra = wave == 0 ? j0 : first_row_at(A.poff, j0, j1, t0);
+      const int64_t rb = wave == SR_WAVES - 1 ? j1 : first_row_at(A.poff, j0, j1, t1);
+      const int64_t eb = A.poff[ra], ee = A.poff[rb];
       if (eb < ee) {
-        const int64_t base0 = eb & ~(int64_t)(SR_K - 1);
-        const uint32_t* ep = A.ent + base0 + SR_K * lane;
-        const uint16_t* hp = A.heads + base0 / SR_K + lane;
-        const int pb = (int)(eb - base0);          // slice = chunk positions [pb, pe)
-        const int pe = (int)(ee - base0);
+        // eb, ee are row starts: multiples of SR_K, so every lane's chunk lies
+        // inside one row and the slice is chunk-aligned
+        const uint32_t* ep = A.ent + eb + SR_K * lane;
+        const uint16_t* hp = A.heads + eb / SR_K + lane;
+        const int pe = (int)(ee - eb);  // slice = chunk positions [0, pe)
         // the slice's first head flag is dropped: its row is cur_row from the start,
         // so every flag seen afterwards closes a row of this slice
         int cur_row = (int)(ra - j0);
@@ -178,55 +184,44 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_gather(SrArgs A, const double* 
         for (int pos = 0; pos < pe; pos += SR_CHUNK) {
           const uint32_t en[SR_K] = {n[0].x, n[0].y, n[0].z, n[0].w, n[1].x, n[1].y, n[1].z, n[1].w,
                                      n[2].x, n[2].y, n[2].z, n[2].w, n[3].x, n[3].y, n[3].z, n[3].w};
-          uint32_t fl = nh;  // bit k: entry k starts a row
+          uint32_t fl = nh & 1u;  // this lane's chunk starts a row
           if (pos + SR_CHUNK < pe) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) n[q] = *reinterpret_cast<const uint4*>(ep + pos + SR_CHUNK + 4 * q);
             nh = hp[(pos + SR_CHUNK) / SR_K];
           }
           const int p0 = pos + SR_K * lane;
-          const bool full = pos > pb && pos + SR_CHUNK < pe;  // wave-uniform
-          double x[SR_K];
-#pragma unroll
-          for (int k = 0; k < SR_K; ++k)  // every entry word (padding included) is inside the row
-            x[k] = LDS_ROW ? *reinterpret_cast<const double*>(reinterpret_cast<const char*>(in_row) + en[k])
-                           : *reinterpret_cast<const double*>(reinterpret_cast<const char*>(row) + en[k]);
-          if (!full) {
-#pragma unroll
-            for (int k = 0; k < SR_K; ++k) {
-              const bool valid = p0 + k > pb - 1 && p0 + k < pe;
-              if (!valid) x[k] = 0.0;
-              if (!valid || p0 + k == pb) fl &= ~(1u << k);
-            }
-          }
-          const int nf = __popc(fl);
-          const int incl = add_scan(nf, lane);
-          const int total = __builtin_amdgcn_readlane(incl, 63);
-          const uint64_t headmask = __ballot(fl != 0);
-          // lane-local walk: every row that ends inside the lane is written
-          // with its lane-local part; the lane's first such row gets the
-          // carry-in added after the scan
-          const int r0 = cur_row + incl - nf;
-          int r = r0;
+          const bool live = p0 < pe;  // lanes past the slice end add zeros to its last row
+          // one row's 16 entries (padding reads the zero slot), summed in entry order
           double p = 0.0;
 #pragma unroll
           for (int k = 0; k < SR_K; ++k) {
-            if (fl & (1u << k)) {
-              out_win[r] = p;
-              ++r;
+            double x;
+            if (LDS_ROW) {
+              x = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(in_row) + en[k]);
+            } else {  // the padding offset is one past the row: read a real element, use 0
+              const uint32_t o = en[k] < pad_off ? en[k] : 0u;
+              x = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(row) + o);
+              if (en[k] >= pad_off) x = 0.0;
             }
-            p = ((fl & (1u << k)) ? 0.0 : p) + x[k];
+            p += x;
           }
-          // p = the lane's trailing segment; lane 0 without a head continues the chunk carry
+          if (!live) p = 0.0;
+          if (!live || p0 == 0) fl = 0u;
+          const int nf = (int)fl;
+          const int incl = add_scan(nf, lane);
+          const int total = __builtin_amdgcn_readlane(incl, 63);
+          const uint64_t headmask = __ballot(fl != 0);
+          // lane 0 without a head continues the row of the previous chunk
           if (lane == 0 && fl == 0) p = chunk_carry + p;
           const uint64_t hb = headmask & below_incl;
           const int seg_start = hb ? 63 - __builtin_clzll(hb) : 0;
           const double S = seg_scan(p, lane, seg_start);
           const double prevS = dpp_f64<0x138>(S);  // wave_shr:1
-          const double carry_in = lane == 0 ? chunk_carry : prevS;
-          if (fl) out_win[r0] = carry_in + out_win[r0];
-          // the lane holding the slice's last entry writes that row (x = 0 past it)
-          if (!full && p0 <= pe - 1 && pe - 1 < p0 + SR_K) out_win[r] = S;
+          const int r = cur_row + incl;            // this lane's row
+          if (fl) out_win[r - 1] = lane == 0 ? chunk_carry : prevS;  // the previous row is complete
+          // the lane holding the slice's last chunk writes that row
+          if (live && p0 + SR_K >= pe) out_win[r] = S;
           const uint64_t Sb = __double_as_longlong(S);
           chunk_carry = __longlong_as_double(
               (long long)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(Sb >> 32), 63) << 32) |
@@ -256,7 +251,7 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_gather(SrArgs A, const double* 
 
 template <bool LDS_ROW, bool PASS2>
 hipError_t launch_pass(const SrArgs& A, const double* src, double* dst, int last, int win, hipStream_t s) {
-  const size_t lds = ((LDS_ROW ? (size_t)A.m : 0) + (size_t)win) * sizeof(double);
+  const size_t lds = ((LDS_ROW ? (size_t)A.m + 1 : 0) + (size_t)win) * sizeof(double);
   hipError_t e = hipFuncSetAttribute((const void*)k_sr_gather<LDS_ROW, PASS2>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -278,31 +273,38 @@ void gw_dev_simrank_release(gw_graph* g) {
   sr_free(g->sr_ent);
   sr_free(g->sr_heads);
   sr_free(g->sr_off);
+  sr_free(g->sr_poff);
   sr_free(g->sr_rows);
   g->sr_n = 0;
   g->sr_m = 0;
 }
 
 // Compact layout (built once per graph on the host): non-isolated vertices
-// in ascending id order, their CSR offsets and head-flagged neighbour ranks.
+// in ascending id order, their CSR offsets, and the row-padded stream of
+// neighbour ranks (each row starts on a 16-entry chunk; padding = 8 * m, the
+// zero slot) with one head bit per chunk.
 static int sr_build_layout(gw_graph* g) {
-  const int64_t n = g->n, nnz = g->nnz;
-  const int64_t padded = ((nnz + SR_K - 1) / SR_K) * SR_K + SR_CHUNK;
+  const int64_t n = g->n;
   std::vector<int32_t> rank((size_t)n, -1), rows;
-  std::vector<int64_t> off(1, 0);
+  std::vector<int64_t> off(1, 0), poff(1, 0);
   rows.reserve((size_t)n);
-  for (int64_t v = 0; v < n; ++v)
-    if (g->offsets[v + 1] > g->offsets[v]) {
+  for (int64_t v = 0; v < n; ++v) {
+    const int64_t d = g->offsets[v + 1] - g->offsets[v];
+    if (d > 0) {
       rank[v] = (int32_t)rows.size();
       rows.push_back((int32_t)v);
       off.push_back(g->offsets[v + 1]);
+      poff.push_back(poff.back() + (d + SR_K - 1) / SR_K * SR_K);
     }
-  std::vector<uint32_t> ent((size_t)padded, 0);
+  }
+  const int64_t m = (int64_t)rows.size();
+  const int64_t padded = poff.back() + SR_CHUNK;  // + one chunk: the one-ahead prefetch stays in bounds
+  std::vector<uint32_t> ent((size_t)padded, (uint32_t)m * (uint32_t)sizeof(double));
   std::vector<uint16_t> heads((size_t)(padded / SR_K), 0);
-  for (int64_t v = 0; v < n; ++v) {
-    const int64_t b = g->offsets[v], e = g->offsets[v + 1];
-    if (e > b) heads[(size_t)(b / SR_K)] |= (uint16_t)(1u << (b % SR_K));
-    for (int64_t k = b; k < e; ++k) ent[k] = (uint32_t)rank[g->nbrs[k]] * (uint32_t)sizeof(double);
+  for (int64_t r = 0; r < m; ++r) {
+    const int64_t v = rows[(size_t)r], b = g->offsets[v], e = g->offsets[v + 1];
+    heads[(size_t)(poff[(size_t)r] / SR_K)] = 1;
+    for (int64_t k = b; k < e; ++k) ent[(size_t)(poff[(size_t)r] + (k - b))] = (uint32_t)rank[g->nbrs[k]] * (uint32_t)sizeof(double);
   }
   auto up = [&](auto*& dptr, const auto& vec) -> bool {
     const size_t bytes = std::max<size_t>(vec.size() * sizeof(vec[0]), 16);
@@ -313,11 +315,12 @@ static int sr_build_layout(gw_graph* g) {
     }
     return vec.empty() || hipMemcpy(dptr, vec.data(), vec.size() * sizeof(vec[0]), hipMemcpyHostToDevice) == hipSuccess;
   };
-  if (!up(g->sr_ent, ent) || !up(g->sr_heads, heads) || !up(g->sr_off, off) || !up(g->sr_rows, rows)) {
+  if (!up(g->sr_ent, ent) || !up(g->sr_heads, heads) || !up(g->sr_off, off) || !up(g->sr_poff, poff) ||
+      !up(g->sr_rows, rows)) {
     g->err = "naive SimRank adjacency layout does not fit in device memory";
     return GW_ERR_NOMEM;
   }
-  g->sr_m = (int64_t)rows.size();
+  g->sr_m = m;
   return GW_OK;
 }
 
@@ -351,13 +354,13 @@ int gw_dev_simrank_naive(gw_graph* g, double C, int iters, double* sim_dev, void
     const unsigned mbk = (unsigned)((m + 255) / 256);
     k_sr_identity<<<mbk, 256, 0, s>>>(m, X);
     GW_HIP_TRY(hipGetLastError());
-    SrArgs A{m, g->sr_off, g->sr_ent, g->sr_heads, C};
-    // input row in LDS when it leaves room for a window of SR_MIN_WIN rows;
-    // the handle's simrank_hbm_row option selects the HBM-row variant (same
-    // bits; tests compare the two)
+    SrArgs A{m, g->sr_off, g->sr_poff, g->sr_ent, g->sr_heads, C};
+    // input row (+ the padding's zero slot) in LDS when it leaves room for a
+    // window of SR_MIN_WIN rows; the handle's simrank_hbm_row option selects
+    // the HBM-row variant (same bits; tests compare the two)
     const int64_t cap = SR_LDS_BYTES / (int64_t)sizeof(double);
-    const bool lds_row = m + SR_MIN_WIN <= cap && !g->opt.simrank_hbm_row;
-    const int win = (int)std::min<int64_t>(m, lds_row ? cap - m : cap);
+    const bool lds_row = m + 1 + SR_MIN_WIN <= cap && !g->opt.simrank_hbm_row;
+    const int win = (int)std::min<int64_t>(m, lds_row ? cap - m - 1 : cap);
     for (int r = 0; r < iters; ++r) {  // while (r++ < STEP), SimRank.java:38
       const int last = r == iters - 1;
       hipError_t e = lds_row ? launch_pass<true, false>(A, X, g->sr_work, 0, win, s)

@@ -68,6 +68,7 @@ def main():
     sh = ctypes.c_void_p(stream.cuda_stream)
     times = {x: [] for x in a.libs}
     steps = {}
+    same = {a.libs[0]: True}
     for rb in range(a.rebuild):
         hs = []
         for name, L in zip(a.libs, libs):
@@ -109,6 +110,19 @@ def main():
                     raise SystemExit(L.gw_last_error(h).decode())
                 times[name].append(e0.elapsed_time(e1))
                 steps[name] = int(cnt[0].item())
+        if rb == 0:  # the variants must emit the same walks (same launch, bitwise)
+            ref = None
+            for L, h, name in zip(libs, hs, a.libs):
+                os.environ.update(envs[libs.index(L)])
+                L.gw_n2v_walks(h, a.L, 7, 0, B, 1, C.ptr(out), None, None, sh)
+                torch.cuda.synchronize()
+                for v in envs[libs.index(L)]:
+                    os.environ.pop(v, None)
+                if ref is None:
+                    ref = out.clone()
+                else:
+                    same[name] = bool(torch.equal(out, ref))
+            del ref
         for L, h in zip(libs, hs):
             L.gw_graph_free(h)
         del out
@@ -119,7 +133,8 @@ def main():
         med = statistics.median(t)
         print(json.dumps({"lib": name, "median_ms": round(med, 3), "min_ms": round(min(t), 3),
                           "max_ms": round(max(t), 3), "n": len(t), "vs_first": round(med / base, 4),
-                          "Gsteps_per_s": round(steps[name] / med / 1e6, 3)}), flush=True)
+                          "Gsteps_per_s": round(steps[name] / med / 1e6, 3),
+                          "walks_equal_first": same.get(name)}), flush=True)
 
 
 if __name__ == "__main__":

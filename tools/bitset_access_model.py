@@ -160,6 +160,8 @@ def main():
                 k = index64(u[1], u[2], d)  # the kernel's 64-bit "other" draw (u.y:u.z)
                 if mode == "region" and k != kp and bounded(u[1], F) in fset:
                     add("sectors_region_membership_word")
+                    if k in cset:  # the candidate's entry, loaded beside the word, is dropped
+                        add("speculative_entry_dropped")
                     if a.tail_list:  # would the candidate's entry (cur -> x) carry a tail-indexed list?
                         x = int(row[k])
                         rx = nbrs[off[x]:off[x + 1]]
