@@ -967,6 +967,23 @@ def run_topsim(R, args, name):
     }
 
 
+LDS_CALIB_FILE = os.path.join(ROOT, "profiles", "r03", "calib_lds.jsonl")
+
+
+def lds_gather_calib(achieved):
+    """The measured ceiling of the gather loop itself (tools/calib/calib_lds.hip:
+    one 1024-thread workgroup per CU, fp64 row in LDS, 4 B offsets streamed 16
+    per lane, random 8 B gathers summed): random-address LDS gathers conflict,
+    so 128 B/clk/CU is not reachable by this access."""
+    try:
+        rows = [json.loads(ln) for ln in open(LDS_CALIB_FILE) if ln.startswith("{")]
+        peak = max(r["gathers_per_s"] for r in rows)
+    except Exception:
+        return None
+    return {"calibrated_peak_gathers_per_s": peak, "frac": achieved / peak,
+            "calib_file": os.path.relpath(LDS_CALIB_FILE, ROOT)}
+
+
 def run_simrank(R, args, name):
     """naive SimRank (SimRank.java) on the GPU: the TopSim ground truth."""
     import numpy as np
@@ -1020,7 +1037,8 @@ def run_simrank(R, args, name):
                    "rounds": rounds, "C": 0.6, "dense_result": f"{V}x{V} fp64"},
         "seconds": sec, "entry_gathers": gathers, "java_neighbour_pairs_per_round": java_pairs,
         "roofline": {"bound": "lds", "achieved": gathers / sec, "peak": lds_peak, "unit": "gathers/s",
-                     "frac": gathers / sec / lds_peak, "traffic": None, "kernel": "k_sr_gather<true,*>"},
+                     "frac": gathers / sec / lds_peak, "traffic": None, "kernel": "k_sr_gather<true,*>",
+                     "random_gather_roofline": lds_gather_calib(gathers / sec)},
         "cpu_baseline": cpu_sr,
     }
 
