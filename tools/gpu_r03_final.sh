@@ -9,6 +9,10 @@ mkdir -p gpurun_out
 TAG=r03f
 KRE="k_walk|k_topsim"
 NOCPU="--no-cpu-baseline"
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t_$TAG.log 2>&1 || { echo TESTS_FAIL; tail -20 gpurun_out/t_$TAG.log; exit 1; }
+echo TESTS_OK; tail -1 gpurun_out/t_$TAG.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo SMOKE_FAIL; tail -5 gpurun_out/smoke_$TAG.log; exit 1; }
+echo SMOKE_OK
 timeout -k 10 500 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo BENCH_FAIL; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 echo BENCH_OK
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o kt -- python bench.py $NOCPU > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.err || { echo PROF_FAIL; tail -20 gpurun_out/prof_$TAG.err; exit 1; }
