@@ -82,6 +82,17 @@ def main():
     ap.add_argument("--hub-bits", type=int, default=0,
                     help="what-if: every entry (u -> x) whose payload has room carries a bitmap of x's "
                          "adjacency to the H highest-degree vertices, answering membership of a hub prev")
+    ap.add_argument("--order", default="id", choices=["id", "degree"],
+                    help="what-if: positions of each row in degree-descending order (ties by id) instead of id "
+                         "order; region slots whose common positions all fall below the payload's bit count "
+                         "become inline ('prefix' mode)")
+    ap.add_argument("--hybrid-prefix", type=int, default=0,
+                    help="what-if (with --order degree): region entries carry a bitset of positions < P and a "
+                         "--tail-filter-bucket filter over positions >= P; selects of the j-th common below the "
+                         "prefix count and membership of k < P are answered in registers")
+    ap.add_argument("--tail-filter", type=int, default=64)
+    ap.add_argument("--hybrid-dir", type=int, default=1,
+                    help="1: entries with 512 < d <= 4096 keep the 128-bit in-entry directory (prefix shrinks by 128)")
     a = ap.parse_args()
     import gwamd
     import oracle
@@ -112,12 +123,16 @@ def main():
         for t in range(2, int(lens[i])):
             prev, cur = int(W[i, t - 2]), int(W[i, t - 1])
             row = nbrs[off[cur]:off[cur + 1]]
+            if a.order == "degree":  # the same multiset, positions re-ranked by degree
+                row = row[np.lexsort((row, -deg[row]))]
             d = len(row)
             prow = nbrs[off[prev]:off[prev + 1]]
-            kp = int(np.searchsorted(row, prev))
+            kp = int(np.nonzero(row == prev)[0][0])
             common = np.nonzero(np.isin(row, prow, assume_unique=True) & (row != prev))[0]
             c = len(common)
             mode = mode_of(c, d, a.list_max, a.payload_bits, a.inline_bits)
+            if mode == "region" and a.order == "degree" and c and int(common.max()) < a.payload_bits - 32:
+                mode = "prefix"  # every common position fits a prefix bitset in the payload: no region reads
             ndir = (d + 511) // 512 if d > 512 else 0
             F = a.filter_dir if 0 < ndir <= a.pdir else a.filter_nodir
             fset = set()
@@ -149,6 +164,11 @@ def main():
                     last_ret = False
                     if r - ap_ < c:
                         add("branch_common")
+                        jsel = min(int(r - ap_), c - 1)
+                        Pp = a.hybrid_prefix if not (a.hybrid_dir and 512 < d <= 4096) else max(a.hybrid_prefix - 128, 0)
+                        if mode == "region" and a.hybrid_prefix and int(common[jsel]) < Pp:
+                            add("select_answered_by_prefix")
+                            break
                         if mode == "region":
                             add("sectors_region_select_block")
                             iters[i] += 1
@@ -158,7 +178,17 @@ def main():
                         break
                     add("branch_other")
                 k = index64(u[1], u[2], d)  # the kernel's 64-bit "other" draw (u.y:u.z)
-                if mode == "region" and k != kp and bounded(u[1], F) in fset:
+                if mode == "region" and a.hybrid_prefix and k != kp:
+                    P = a.hybrid_prefix if not (a.hybrid_dir and 512 < d <= 4096) else max(a.hybrid_prefix - 128, 0)
+                    if k < P:
+                        add("membership_answered_by_prefix")
+                    else:  # tail filter: buckets over positions P..d-1
+                        tail = [int(x) for x in common if x >= P]
+                        TB = a.tail_filter
+                        b = (k - P) * TB // max(d - P, 1)
+                        if any((x - P) * TB // max(d - P, 1) == b for x in tail):
+                            add("sectors_region_membership_word")
+                elif mode == "region" and k != kp and bounded(u[1], F) in fset:
                     add("sectors_region_membership_word")
                     if k in cset:  # the candidate's entry, loaded beside the word, is dropped
                         add("speculative_entry_dropped")
