@@ -83,11 +83,11 @@ def main():
                     help="what-if: every entry (u -> x) whose payload has room carries a bitmap of x's "
                          "adjacency to the H highest-degree vertices, answering membership of a hub prev")
     ap.add_argument("--order", default="id", choices=["id", "degree"],
-                    help="what-if: positions of each row in degree-descending order (ties by id) instead of id "
-                         "order; region slots whose common positions all fall below the payload's bit count "
-                         "become inline ('prefix' mode)")
+                    help="what-if: positions of each row in degree-descending order, ties by id, instead of id "
+                         "order")
     ap.add_argument("--hybrid-prefix", type=int, default=0,
-                    help="what-if (with --order degree): region entries carry a bitset of positions < P and a "
+                    help="what-if (with --order degree): region slots whose commons all lie below the payload's "
+                         "bit count become inline ('prefix' mode); the others carry a bitset of positions < P and a "
                          "--tail-filter-bucket filter over positions >= P; selects of the j-th common below the "
                          "prefix count and membership of k < P are answered in registers")
     ap.add_argument("--tail-filter", type=int, default=64)
@@ -131,7 +131,7 @@ def main():
             common = np.nonzero(np.isin(row, prow, assume_unique=True) & (row != prev))[0]
             c = len(common)
             mode = mode_of(c, d, a.list_max, a.payload_bits, a.inline_bits)
-            if mode == "region" and a.order == "degree" and c and int(common.max()) < a.payload_bits - 32:
+            if mode == "region" and a.hybrid_prefix and c and int(common.max()) < a.payload_bits - 32:
                 mode = "prefix"  # every common position fits a prefix bitset in the payload: no region reads
             ndir = (d + 511) // 512 if d > 512 else 0
             F = a.filter_dir if 0 < ndir <= a.pdir else a.filter_nodir
