@@ -605,7 +605,12 @@ static bool listed_pays(gw_graph* g, double q) {
   // p = 0.25, q = 4: 53.0 vs 52.6 ms per 5.1e8 steps)
   if (q >= 1.0) return false;
   const double save_s = (double)g->opt.expected_steps * (0.46 / 4.9e10);
-  return save_s > gw_bitset_build_model_s(g);
+  const double build_s = gw_bitset_build_model_s(g);
+  if (build_s < 0) {  // the model run failed on the device: keep the plain entries
+    (void)hipGetLastError();
+    return false;
+  }
+  return save_s > build_s;
 }
 
 // bitset walk time per step (R-MAT-20 headline 3.2e10 walk-steps/s) and the
@@ -619,7 +624,7 @@ static int n2v_prepare_auto(gw_graph* g, double p, double q) {
                      g->nnz > 0 && g->nnz < (int64_t)0xFFFFFFFF;
   auto bitset_or_rejection = [&]() {
     int rc = gw_dev_n2v_prepare(g, p, q, GW_N2V_BITSET);
-    if (rc == GW_ERR_CAPACITY || rc == GW_ERR_NOMEM) {
+    if (rc == GW_ERR_CAPACITY || rc == GW_ERR_NOMEM || rc == GW_ERR_UNSUPPORTED) {
       (void)hipGetLastError();
       g->err.clear();
       rc = gw_dev_n2v_prepare(g, p, q, GW_N2V_REJECTION);
@@ -629,8 +634,18 @@ static int n2v_prepare_auto(gw_graph* g, double p, double q) {
   if (!bs_ok) return gw_dev_n2v_prepare(g, p, q, GW_N2V_REJECTION);
   const int64_t steps = g->opt.expected_steps;
   if (steps <= 0) return bitset_or_rejection();
+  // the pilot needs the plain rejection sampler only: its trial count does
+  // not depend on listed entries, so their build is deferred until rejection
+  // is the final choice (and then only when listed_pays)
+  const int32_t listed_opt = g->opt.listed;
+  g->opt.listed = 0;
   int rc = gw_dev_n2v_prepare(g, p, q, GW_N2V_REJECTION);
+  g->opt.listed = listed_opt;
   if (rc != GW_OK) return rc;
+  auto keep_rejection = [&]() {
+    if (listed_opt != 0 && listed_pays(g, q)) return gw_dev_n2v_prepare(g, p, q, GW_N2V_REJECTION);
+    return GW_OK;
+  };
   // pilot: the rejection sampler's own walks (65,536 walks of length 80 from
   // iteration 0's shuffled starts, a fixed internal seed) counting its trials
   // per step; the modelled time per trial is measured (R-MAT-20 p = 0.25
@@ -652,11 +667,12 @@ static int n2v_prepare_auto(gw_graph* g, double p, double q) {
   dev_free(buf);
   dev_free(cnt);
   (void)hipGetLastError();
-  if (t_rej < 0) return GW_OK;  // no pilot: keep the rejection sampler
+  if (t_rej < 0) return keep_rejection();  // no pilot: keep the rejection sampler
   const double build = gw_bitset_build_model_s(g);
+  (void)hipGetLastError();
   const double bitset_s = build + (double)steps * kBitsetStepSeconds;
   const double rejection_s = (double)steps * t_rej;
-  if (build < 0 || bitset_s >= rejection_s) return GW_OK;
+  if (build < 0 || bitset_s >= rejection_s) return keep_rejection();
   return bitset_or_rejection();
 }
 
@@ -763,7 +779,7 @@ int gw_dev_n2v_prepare(gw_graph* g, double p, double q, int mode) {
     rc = gw_dev_bitset_build(g, table_budget(g), true);
     if (rc == GW_OK) {
       listed = true;
-    } else if (rc == GW_ERR_CAPACITY || rc == GW_ERR_NOMEM) {
+    } else if (rc == GW_ERR_CAPACITY || rc == GW_ERR_NOMEM || rc == GW_ERR_UNSUPPORTED) {
       gw_dev_bitset_release(g);
       (void)hipGetLastError();
       g->err.clear();
@@ -993,6 +1009,52 @@ int gw_dev_n2v_walks(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int6
   }
 #undef GW_LAUNCH
   GW_HIP_TRY(hipGetLastError());
+  return GW_OK;
+}
+
+__global__ void k_philox(const uint32_t* __restrict__ in, int64_t n, uint32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* a = in + 6 * i;
+  const gw_u4 r = gw_philox(a[0], a[1], a[2], a[3], a[4], a[5]);
+  uint32_t* o = out + 4 * i;
+  o[0] = r.x;
+  o[1] = r.y;
+  o[2] = r.z;
+  o[3] = r.w;
+}
+
+extern "C" int gw_philox4x32(int device, const uint32_t* in, int64_t n, uint32_t* out) {
+  if (n < 0 || (n > 0 && (!in || !out))) return gw_fail(nullptr, GW_ERR_INVALID, "bad arrays");
+  if (n == 0) return GW_OK;
+  if (device < 0) {  // host evaluation of the same header
+    for (int64_t i = 0; i < n; ++i) {
+      const uint32_t* a = in + 6 * i;
+      const gw_u4 r = gw_philox(a[0], a[1], a[2], a[3], a[4], a[5]);
+      out[4 * i] = r.x;
+      out[4 * i + 1] = r.y;
+      out[4 * i + 2] = r.z;
+      out[4 * i + 3] = r.w;
+    }
+    return GW_OK;
+  }
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+    return gw_fail(nullptr, GW_ERR_DEVICE, "no HIP device visible (libgraphwalk has no CPU fallback)");
+  if (device >= count) return gw_fail(nullptr, GW_ERR_INVALID, "device ordinal out of range");
+  GW_GUARD_DEVICE(nullptr, device);
+  uint32_t *d_in = nullptr, *d_out = nullptr;
+  hipError_t e = hipMalloc((void**)&d_in, sizeof(uint32_t) * 6 * (size_t)n);
+  if (e == hipSuccess) e = hipMalloc((void**)&d_out, sizeof(uint32_t) * 4 * (size_t)n);
+  if (e == hipSuccess) e = hipMemcpy(d_in, in, sizeof(uint32_t) * 6 * (size_t)n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    k_philox<<<grid_for(n), kBlock>>>(d_in, n, d_out);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out, d_out, sizeof(uint32_t) * 4 * (size_t)n, hipMemcpyDeviceToHost);
+  if (d_in) (void)hipFree(d_in);
+  if (d_out) (void)hipFree(d_out);
+  if (e != hipSuccess) return gw_fail(nullptr, GW_ERR_DEVICE, "%s", hipGetErrorString(e));
   return GW_OK;
 }
 

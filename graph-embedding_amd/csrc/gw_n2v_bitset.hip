@@ -1411,15 +1411,39 @@ void gw_dev_bitset_release(gw_graph* g) {
   bs_free(g->d.bs_nbr);
 }
 
+// row holding adjacency slot e (upper bound over offsets)
+__device__ __forceinline__ int64_t bs_row_of(const gw_dev_graph& G, int64_t e) {
+  int64_t lo = 0, hi = G.n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (G.offsets[mid + 1] <= e)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
 // sum over undirected edges of min(deg u, deg v) = k_bs_tri's probes (each
-// edge counted at its owner u, where min = deg v)
+// edge counted at its owner u, where min = deg v).  Edge-centric: a thread
+// takes kWorkChunk consecutive slots (one row search per row it enters), so a
+// hub's row is spread over many threads instead of one serial loop.
+constexpr int kWorkChunk = 16;
 __global__ void k_bs_work(gw_dev_graph G, unsigned long long* __restrict__ acc) {
-  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kWorkChunk;
   unsigned long long w = 0;
-  if (u < G.n) {
-    const int64_t ub = G.offsets[u], du = G.offsets[u + 1] - ub;
-    for (int64_t j = 0; j < du; ++j) {
-      const int32_t v = G.nbrs[ub + j];
+  if (e0 < G.nnz) {
+    const int64_t e1 = e0 + kWorkChunk < G.nnz ? e0 + kWorkChunk : G.nnz;
+    int64_t u = bs_row_of(G, e0);
+    int64_t ue = G.offsets[u + 1];
+    int64_t du = ue - G.offsets[u];
+    for (int64_t e = e0; e < e1; ++e) {
+      if (e >= ue) {
+        u = bs_row_of(G, e);
+        ue = G.offsets[u + 1];
+        du = ue - G.offsets[u];
+      }
+      const int32_t v = G.nbrs[e];
       const int64_t dv = G.deg[v];
       if (du > dv || (du == dv && u <= v)) w += (unsigned long long)dv;
     }
@@ -1450,10 +1474,17 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
              std::to_string(budget_bytes) + " B budget: use GW_N2V_REJECTION";
     return GW_ERR_CAPACITY;
   }
+  // a REGION entry packs its directory block count in meta bits 16.. (about
+  // deg / 8192); past 2^27 it would reach kMetaDual / kMetaStash (bits 30, 31)
+  if (g->max_degree >= ((int64_t)1 << 27)) {
+    g->err = "bitset mode supports vertex degrees < 2^27: use GW_N2V_REJECTION";
+    return GW_ERR_UNSUPPORTED;
+  }
   int rc;
   uint64_t* sz = nullptr;
   uint64_t* roff = nullptr;
   int32_t *ids = nullptr, *order = nullptr;
+  int32_t* dkey = nullptr;  // sorted degrees (discarded)
   uint32_t* nit = nullptr;
   uint32_t* itoff = nullptr;
   TriItem* items = nullptr;
@@ -1467,6 +1498,7 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
     bs_free(itoff);
     bs_free(items);
     bs_free(tmp);
+    bs_free(dkey);
   };
   auto fail = [&](int code) {
     cleanup();
@@ -1494,7 +1526,6 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
                                                       (const int32_t*)nullptr, (int32_t*)nullptr, (int)n));
   BS_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, nit, itoff, (int)(n + 1)));
   if ((rc = bs_alloc(g, (char**)&tmp, (int64_t)std::max(tb, tb2) + 1))) return fail(rc);
-  int32_t* dkey = nullptr;  // sorted degrees (discarded)
   if ((rc = bs_alloc(g, &dkey, n))) return fail(rc);
   BS_TRY(hipcub::DeviceRadixSort::SortPairsDescending(tmp, tb, d.deg, dkey, ids, order, (int)n));
   // diagnostics build (GW_DIAG_BS_FILL & 8): both passes launched as two
@@ -1583,8 +1614,9 @@ double gw_bitset_build_model_s(gw_graph* g) {
   if (hipMalloc((void**)&acc, sizeof(unsigned long long)) != hipSuccess) return -1.0;
   unsigned long long w = 0;
   bool ok = hipMemset(acc, 0, sizeof w) == hipSuccess;
-  if (ok && g->n > 0) {
-    k_bs_work<<<(unsigned)((g->n + kB - 1) / kB), kB>>>(g->d, acc);
+  if (ok && g->nnz > 0) {
+    const int64_t threads = (g->nnz + kWorkChunk - 1) / kWorkChunk;
+    k_bs_work<<<(unsigned)((threads + kB - 1) / kB), kB>>>(g->d, acc);
     ok = hipGetLastError() == hipSuccess;
   }
   ok = ok && hipMemcpy(&w, acc, sizeof w, hipMemcpyDeviceToHost) == hipSuccess;

@@ -114,19 +114,6 @@ __device__ __forceinline__ double seg_scan(double S, int lane, int seg) {
   return S;
 }
 
-// Inclusive sum over lanes [0, l] of ints.
-__device__ __forceinline__ int add_scan(int P, int lane) {
-  const int r = lane & 15;
-  int t;
-  t = dpp_i32<0x111>(P); if (r >= 1) P += t;
-  t = dpp_i32<0x112>(P); if (r >= 2) P += t;
-  t = dpp_i32<0x114>(P); if (r >= 4) P += t;
-  t = dpp_i32<0x118>(P); if (r >= 8) P += t;
-  t = dpp_i32<0x142, 0xA>(P); if (lane & 16) P += t;
-  t = dpp_i32<0x143, 0xC>(P); if (lane >= 32) P += t;
-  return P;
-}
-
 // One workgroup per row i of `src`.  The rows j are processed in windows of
 // `win` rows whose totals land in an LDS window (no global stores inside
 // the entry loop, so the one-chunk-ahead prefetch is never held up behind
@@ -208,10 +195,13 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_gather(SrArgs A, const double* 
           }
           if (!live) p = 0.0;
           if (!live || p0 == 0) fl = 0u;
-          const int nf = (int)fl;
-          const int incl = add_scan(nf, lane);
-          const int total = __builtin_amdgcn_readlane(incl, 63);
+          // heads at or below this lane: v_mbcnt over the head ballot (exclusive
+          // count) + this lane's own flag, instead of a 6-step DPP scan
           const uint64_t headmask = __ballot(fl != 0);
+          const int incl = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(headmask >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)headmask, 0u)) +
+                           (int)fl;
+          const int total = __popcll(headmask);
           // lane 0 without a head continues the row of the previous chunk
           if (lane == 0 && fl == 0) p = chunk_carry + p;
           const uint64_t hb = headmask & below_incl;

@@ -100,6 +100,7 @@ SIGNATURES = {
     "gw_last_error": (CP, [P]),
     "gw_strerror": (CP, [ctypes.c_int]),
     "gw_device_count": (ctypes.c_int, [PI32]),
+    "gw_philox4x32": (ctypes.c_int, [ctypes.c_int, P, I64, P]),
     "gw_graph_load_edgelist": (ctypes.c_int, [CP, CP, ctypes.c_int, ctypes.c_int, ctypes.c_int, I64, PP]),
     "gw_graph_from_edges": (ctypes.c_int, [I64, P, P, P, ctypes.c_int, ctypes.c_int, I64, PP]),
     "gw_graph_from_csr": (ctypes.c_int, [I64, P, P, P, P, P, ctypes.c_int, ctypes.c_int, PP]),

@@ -104,23 +104,52 @@ def _scale(args):
     # the walks this rank will run on this preparation: the sampler's optional
     # tables are built only when they pay back within them (gw_options_t)
     g.options(expected_steps=gd.shard_range(args.num_walks * g.n, world, rank)[1] * (args.walk_length - 1))
+    if world > 1:
+        import torch.distributed as dist
+        dev = torch.device("cuda", device) if args.dist_backend == "nccl" else torch.device("cpu")
+    err = None
     if args.sampler == "auto":
         # the library picks bitset or rejection by modelled end-to-end time for
         # the walks announced above (the rejection sampler's pilot trials
         # against the bitset build model); with several ranks rank 0 decides
-        # for all, so every shard comes from the same sampler
+        # for all, so every shard comes from the same sampler.  A failure on
+        # rank 0 is broadcast as mode -2 so no rank waits in a collective for it.
+        chosen = -1
         if world == 1 or rank == 0:
-            C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, C.N2V_AUTO), g.handle)
+            try:
+                C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, C.N2V_AUTO), g.handle)
+                chosen = g.info().n2v_mode
+            except Exception as e:  # noqa: BLE001 - re-raised below on every rank
+                if world == 1:
+                    raise
+                err, chosen = e, -2
         if world > 1:
-            import torch.distributed as dist
-            dev = torch.device("cuda", device) if args.dist_backend == "nccl" else torch.device("cpu")
-            m = torch.tensor([g.info().n2v_mode if rank == 0 else -1], dtype=torch.int64, device=dev)
+            m = torch.tensor([chosen if rank == 0 else -1], dtype=torch.int64, device=dev)
             dist.broadcast(m, 0)
-            if rank != 0:
-                C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, int(m.item())), g.handle)
+            chosen = int(m.item())
+            if chosen == -2 and err is None:
+                err = RuntimeError("rank 0 failed to prepare the sampler (GW_N2V_AUTO)")
+            if rank != 0 and err is None:
+                try:
+                    C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, chosen), g.handle)
+                except Exception as e:  # noqa: BLE001
+                    err = e
     else:
         mode = C.N2V_BITSET if args.sampler == "bitset" else C.N2V_REJECTION
-        C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, mode), g.handle)
+        try:
+            C.check(C.lib().gw_n2v_prepare(g.handle, args.p, args.q, mode), g.handle)
+        except Exception as e:  # noqa: BLE001
+            if world == 1:
+                raise
+            err = e
+    if world > 1:
+        # every rank prepared (or every rank raises): no rank enters the walk
+        # all-gather while another has already failed
+        ok = torch.tensor([0 if err is not None else 1], dtype=torch.int64, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            dist.destroy_process_group()
+            raise err if err is not None else RuntimeError("another rank failed to prepare the sampler")
     nwalks = args.num_walks * g.n
     L = args.walk_length
     begin, count = gd.shard_range(nwalks, world, rank)

@@ -15,8 +15,12 @@ advance exactly as the reference's would.  The uniforms are generated on the
 host by numpy (they ARE the reference's stream), the walks and alias tables
 are computed by the HIP kernels of libgraphwalk.
 
-`mode="scale"` instead runs the Philox/rejection-sampling kernel (no per-edge
-tables; reproducible by `seed`, identical for any GPU count).
+`mode="scale"` instead runs the Philox-keyed scale samplers (reproducible by
+`seed`, identical for any GPU count).  `preprocess_transition_probs` then only
+uploads the graph: the sampler is prepared by the first `simulate_walks`, once
+num_walks * n * (walk_length - 1) steps are known, with GW_N2V_AUTO by default
+(the per-edge bitset sampler when its build pays back over those steps, else
+the rejection sampler; `sampler="bitset"` / `"rejection"` force one).
 """
 import random
 from collections.abc import Mapping
@@ -79,7 +83,10 @@ class _AliasEdges(Mapping):
 class Graph:
     """node2vec.Graph (node2vec.py:6-113) on the GPU."""
 
-    def __init__(self, nx_G, is_directed, p, q, device=0, mode="replay", seed=0):
+    def __init__(self, nx_G, is_directed, p, q, device=0, mode="replay", seed=0, sampler="auto"):
+        if sampler not in ("auto", "bitset", "rejection"):
+            raise ValueError("sampler must be 'auto', 'bitset' or 'rejection'")
+        self.sampler = sampler
         self.G = nx_G
         self.is_directed = is_directed
         self.p = p
@@ -102,11 +109,16 @@ class Graph:
 
     # -- node2vec.py:83-113 ----------------------------------------------------
     def preprocess_transition_probs(self):
-        mode = C.N2V_REPLAY if self.mode == "replay" else C.N2V_REJECTION
         self._g.to_device(self.device)
+        self._prepared = True
+        if self.mode != "replay":
+            # scale mode: the sampler is chosen and built by the first
+            # simulate_walks, when the number of walk steps is known
+            self._scale_mode = None
+            return
+        mode = C.N2V_REPLAY
         C.check(C.lib().gw_n2v_prepare(self._g.handle, float(self.p), float(self.q), mode),
                 self._g.handle)
-        self._prepared = True
         if mode == C.N2V_REPLAY:
             inf = self._g.info()
             nnz, E = inf.nnz, inf.edge_alias_entries
@@ -162,10 +174,26 @@ class Graph:
         lab = self._csr["labels"]
         return [lab[out[i, :lens[i]]].tolist() for i in range(nw)]
 
+    @property
+    def scale_sampler(self):
+        """GW_N2V_* the scale sampler was prepared with (None before the first
+        simulate_walks)."""
+        return getattr(self, "_scale_mode", None)
+
+    def _prepare_scale(self, steps):
+        if self._scale_mode is not None:
+            return
+        mode = {"auto": C.N2V_AUTO, "bitset": C.N2V_BITSET, "rejection": C.N2V_REJECTION}[self.sampler]
+        self._g.options(expected_steps=int(steps))
+        h = self._g.handle
+        C.check(C.lib().gw_n2v_prepare(h, float(self.p), float(self.q), mode), h)
+        self._scale_mode = self._g.info().n2v_mode
+
     def _simulate_scale(self, num_walks, walk_length):
         import torch
         n = self._csr["labels"].shape[0]
         nw = num_walks * n
+        self._prepare_scale(nw * max(int(walk_length) - 1, 0))
         dev = torch.device("cuda", self.device)
         out = torch.empty((nw, walk_length), dtype=torch.int32, device=dev)
         lens = torch.empty(nw, dtype=torch.int32, device=dev)

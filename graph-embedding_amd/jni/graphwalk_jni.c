@@ -224,35 +224,3 @@ JNIEXPORT void JNICALL Java_simrank_GraphWalkNative_simrankNaive(JNIEnv* env, jc
   (*env)->ReleaseDoubleArrayElements(env, out, sim, 0);
   if (rc != GW_OK) throw_gw(env, rc, g);
 }
-
-/* utils.Print.printByOrder (Print.java:25-53) layout from top-k rows as topsimTopK returns them (score desc,
- * id asc): NOT the reference's bytes when rows have ties or fewer than k nonzeros — topsimWriteText is */
-JNIEXPORT void JNICALL Java_simrank_GraphWalkNative_writeTopK(JNIEnv* env, jclass cls, jstring path, jintArray ids,
-                                                              jdoubleArray scores, jintArray rowIds, jint k,
-                                                              jstring sep) {
-  (void)cls;
-  if (!path || !ids || !scores || !rowIds || !sep || k < 0) {
-    throw_arg(env, "null argument or k < 0");
-    return;
-  }
-  const jsize nr = (*env)->GetArrayLength(env, rowIds);
-  const int64_t need = (int64_t)nr * (int64_t)k;
-  if ((int64_t)(*env)->GetArrayLength(env, ids) < need || (int64_t)(*env)->GetArrayLength(env, scores) < need) {
-    throw_arg(env, "ids / scores shorter than rowIds.length * k");
-    return;
-  }
-  const char* p = (*env)->GetStringUTFChars(env, path, 0);
-  const char* s = p ? (*env)->GetStringUTFChars(env, sep, 0) : NULL;
-  jint* id = s ? (*env)->GetIntArrayElements(env, ids, 0) : NULL;
-  jdouble* sc = id ? (*env)->GetDoubleArrayElements(env, scores, 0) : NULL;
-  jint* rid = sc ? (*env)->GetIntArrayElements(env, rowIds, 0) : NULL;
-  int rc = GW_ERR_NOMEM;
-  if (rid) rc = gw_write_sim_text_topk(p, (const int32_t*)id, sc, (const int32_t*)rid, nr, k, s, 6);
-  if (id) (*env)->ReleaseIntArrayElements(env, ids, id, JNI_ABORT);
-  if (sc) (*env)->ReleaseDoubleArrayElements(env, scores, sc, JNI_ABORT);
-  if (rid) (*env)->ReleaseIntArrayElements(env, rowIds, rid, JNI_ABORT);
-  if (s) (*env)->ReleaseStringUTFChars(env, sep, s);
-  if (p) (*env)->ReleaseStringUTFChars(env, path, p);
-  if ((*env)->ExceptionCheck(env)) return;
-  if (rc != GW_OK) throw_gw(env, rc, NULL);
-}

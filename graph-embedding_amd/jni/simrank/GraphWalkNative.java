@@ -45,8 +45,4 @@ public final class GraphWalkNative {
     public static native void topsimWriteText(long g, int variant, int sample, int step, double C, long seed,
                                               int[] sources, int topk, String path, String separator, long[] stats)
             throws java.io.IOException;
-
-    /** Print.printByOrder layout from topsimTopK rows (score desc, id asc; not Java's tie order). */
-    public static native void writeTopK(String path, int[] ids, double[] scores, int[] rowIds, int k,
-                                        String separator);
 }

@@ -153,6 +153,15 @@ const char* gw_last_error(const gw_graph* g);
 const char* gw_strerror(int code);
 /* number of visible GPUs (0 and GW_ERR_DEVICE when none)                    */
 int gw_device_count(int* count);
+/* The counter-based generator behind every scale-mode draw (Philox4x32-10,
+ * Salmon et al. SC'11; csrc/gw_philox.h), so a host can reproduce the walks'
+ * and TopSim's draws: for i < n, in[6i..6i+5] = (c0, c1, c2, c3, k0, k1) ->
+ * out[4i..4i+3] = (x, y, z, w).  device >= 0 evaluates the kernels' own
+ * device build on that GPU; device = -1 evaluates the same source on the host
+ * (no GPU needed).  Replaces no reference symbol (the reference draws from
+ * np.random / java.util.Random streams, node2vec.py:156-157, Graph.java:17);
+ * pinned to Random123's published known-answer vectors (tests).            */
+int gw_philox4x32(int device, const uint32_t* in, int64_t n, uint32_t* out);
 
 /* ---- graph construction (host) ------------------------------------------ */
 /* Replaces read_graph (node2vec/src/main.py:76-89, sem NX_SIMPLE) and

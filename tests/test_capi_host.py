@@ -476,7 +476,10 @@ def test_jni_shim_calls_only_exported_abi(gw):
     untested here): every gw_* function it calls is declared in
     include/graphwalk.h and exported by libgraphwalk.so, and every native
     method of simrank.GraphWalkNative has its Java_simrank_GraphWalkNative_* C
-    definition."""
+    definition.  Every Java-facing writer must emit Print.printByOrder's bytes
+    (Print.java:25-53, FixedMaxPQ.java:30-39, 72-76): the shim may reach the
+    sim-file writers only through gw_topsim_write_text (sparse rows, FixedMaxPQ
+    replayed), never the score-desc/id-asc top-k writer."""
     from gwamd import _lib as C
     jni = open(os.path.join(ROOT, "graph-embedding_amd", "jni", "graphwalk_jni.c")).read()
     hdr = open(os.path.join(ROOT, "include", "graphwalk.h")).read()
@@ -490,3 +493,6 @@ def test_jni_shim_calls_only_exported_abi(gw):
     natives = set(re.findall(r"public static native \w+ (\w+)\(", java))
     defined = set(re.findall(r"Java_simrank_GraphWalkNative_(\w+)\(", jni))
     assert natives and natives == defined, (natives, defined)
+    writers = {f for f in called if f.startswith("gw_write_sim_text") or f.endswith("write_text")}
+    assert writers == {"gw_topsim_write_text"}, writers
+    assert "writeTopK" not in natives

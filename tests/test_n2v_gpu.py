@@ -586,6 +586,32 @@ def test_cli_scale_two_ranks_equal_one(gw, tmp_path):
     assert one.read_bytes() == two.read_bytes()
 
 
+@pytest.mark.parametrize("sampler", ["auto", "rejection"])
+def test_cli_scale_two_ranks_fail_together(gw, tmp_path, sampler):
+    """A prepare that fails (p = 0: node2vec.py:70-76 divides by p) makes
+    EVERY rank raise, promptly: under --sampler auto rank 0 broadcasts the
+    failure sentinel instead of a mode, otherwise the ranks all-reduce a
+    success flag before any walk collective (the other ranks used
+    to wait in a collective until the NCCL timeout)."""
+    import socket
+    import subprocess
+    import sys
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "graph-embedding_amd")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, PYTHONPATH=pkg + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "gwamd.cli",
+                        "--input", os.path.join(DATA, "karate.edgelist"), "--delimiter", " ", "--p", "0",
+                        "--q", "4", "--mode", "scale", "--sampler", sampler, "--num-walks", "1",
+                        "--walks", str(tmp_path / "w.txt"), "--dist-backend", "gloo"],
+                       env=env, capture_output=True, text=True, timeout=150)
+    assert r.returncode != 0
+    assert r.stderr.count("p and q must be > 0") + r.stderr.count("failed to prepare") >= 2, r.stderr[-3000:]
+    assert not (tmp_path / "w.txt").exists()
+
+
 @pytest.mark.parametrize("mode", ["bitset", "rejection"])
 def test_walks_host_pipeline_equals_device(gw, mode, monkeypatch):
     """gw_n2v_walks_host (chunked, kernel/copy overlapped on two streams):
@@ -732,3 +758,38 @@ def test_auto_sampler_choice_by_end_to_end_model(gw):
     G.options(expected_steps=10**14)
     C.check(C.lib().gw_n2v_prepare(G.handle, 0.25, 4.0, C.N2V_REJECTION), G.handle)
     assert G.info().listed == 0
+
+
+def test_dropin_scale_mode_routes_through_auto(gw, oracle):
+    """node2vec.Graph(..., mode="scale") defers the sampler to simulate_walks
+    and prepares it with GW_N2V_AUTO for num_walks * n * (L - 1) steps
+    (node2vec.py:83-113 then :41-59): at q = 4 with enough walks to pay the
+    build back it takes the bitset sampler and returns exactly the bitset
+    walks (== oracle); sampler="rejection" forces the rejection walks."""
+    import networkx as nx
+    from gwamd import _lib as C
+    from gwamd import node2vec
+    nxg = nx.read_edgelist(os.path.join(DATA, "moreno_crime_crime.txt"), nodetype=int, create_using=nx.DiGraph(),
+                           delimiter="\t")
+    for e in nxg.edges():
+        nxg[e[0]][e[1]]["weight"] = 1
+    nxg = nxg.to_undirected()
+    n, L, r = nxg.number_of_nodes(), 40, 200
+    G = node2vec.Graph(nxg, False, 0.25, 4.0, mode="scale", seed=11)
+    G.preprocess_transition_probs()
+    assert G.scale_sampler is None  # nothing built before the step count is known
+    walks = G.simulate_walks(r, L)
+    assert G.scale_sampler == C.N2V_BITSET
+    assert G._g.options()["expected_steps"] == r * n * (L - 1)
+    csr = G._g.export_csr()
+    lab = csr["labels"]
+    ref, rl, _ = oracle.walks_bitset(csr, 0.25, 4.0, 11, L, 0, r * n, nthreads=4)
+    assert len(walks) == r * n
+    for i in (0, 1, n, r * n // 2, r * n - 1):
+        assert walks[i] == lab[ref[i, :rl[i]]].tolist()
+    R = node2vec.Graph(nxg, False, 0.25, 4.0, mode="scale", seed=11, sampler="rejection")
+    R.preprocess_transition_probs()
+    wr = R.simulate_walks(2, L)
+    assert R.scale_sampler == C.N2V_REJECTION
+    ref2, rl2, _ = oracle.walks_scale(dict(csr, weights=None), 0.25, 4.0, 11, L, 0, 2 * n, nthreads=4)
+    assert [lab[ref2[i, :rl2[i]]].tolist() for i in range(2 * n)] == wr
