@@ -207,6 +207,10 @@ struct N2VParams {
   uint32_t k0, k1;   // step key
   uint32_t pk0, pk1; // permutation key
   uint32_t diag;     // timing experiments only (GW_DIAG_NO_STORE=1: no walk output stores)
+  // mixture proposal (unweighted undirected, q > 1; see k_walk_scale)
+  double mix_o;       // outlier mass of the return edge: max(0, 1/p - 1/q)
+  double mix_p;       // mass per vertex of the prev branch: 1 - 1/q
+  double mix_prev;    // acceptance of prev drawn by the cur branch: min(1, (1/p) / (1/q))
 };
 
 template <bool WEIGHTED>
@@ -298,7 +302,22 @@ constexpr int kStage = 16;
 // runtime test: with both paths in one body the compiler merges the two
 // neighbour-id loads into one dword load after the entry's dwordx3, which
 // serialises two dependent requests per step.
-template <bool FIRST_ORDER, bool WEIGHTED, bool DIRECTED, bool ENT>
+//
+// MIX (unweighted, undirected, q > 1): the target weights over x in N(cur)
+// (node2vec.py:61-81) are w(prev) = 1/p, w(x) = 1 for x in N(prev), 1/q
+// otherwise, i.e.  w = 1/q * [x in N(cur)] + (1 - 1/q) * [x in N(prev)]
+// (+ the return edge's own weight).  Sampling that mixture directly needs no
+// envelope: with mass d_cur/q pick x uniformly from N(cur) and accept it (no
+// has_edge probe), with mass (1 - 1/q) * d_prev pick x uniformly from N(prev)
+// and accept it iff x is in N(cur) (one probe of cur's neighbour set; x ==
+// prev, a self-loop of prev, is rejected), with mass max(0, 1/p - 1/q) return
+// to prev (an outlier; when 1/p < 1/q a prev drawn from N(cur) is accepted
+// with probability q/p).  Every x then has accepted mass exactly w(x).  Per
+// step it costs (d_cur/q + 2 (1 - 1/q) d_prev) / Z requests against
+// d_cur (2 - 1/q) / Z for the uniform-proposal rejection below (Z = sum of
+// w), so a step takes the mixture iff d_prev < d_cur — known before the first
+// draw, so the choice is a pure function of the walk (oracle: or_walks_scale).
+template <bool FIRST_ORDER, bool WEIGHTED, bool DIRECTED, bool ENT, bool MIX = false>
 __global__ void __launch_bounds__(kBlock)
 k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_count,
              int shuffle, int32_t* __restrict__ out, int32_t* __restrict__ lens,
@@ -359,6 +378,34 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
           next = G.nbrs[slot];
         }
         acc = true;
+      } else if (MIX && pe - pb < d) {  // mixture proposal (see above)
+        const gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
+        ++trial;
+        const int64_t dp = pe - pb;
+        const double Ac = (double)d * P.a_q;
+        const double H = P.mix_o + Ac + (double)dp * P.mix_p;
+        const double r = gw_u01(u.z) * H;
+        if (r < P.mix_o) {  // return-edge outlier
+          slot = -1;
+          next = prev;
+          acc = true;
+        } else {
+          const bool from_cur = r < P.mix_o + Ac;
+          slot = (from_cur ? b : pb) + (int64_t)gw_index(u.x, u.y, (uint32_t)(from_cur ? d : dp));
+          if (ENT) {  // the slot entry (of cur's or prev's row) carries the candidate's row
+            const gw_ts_ent en = gw_ts_load(G.sent + slot);
+            next = en.x;
+            nb = en.off;
+            nd = en.d;
+          } else {
+            next = G.nbrs[slot];
+          }
+          if (from_cur)
+            acc = next != prev || gw_u01(u.w) < P.mix_prev;
+          else
+            acc = next != prev && gw_has_edge(G, b, e, next);  // x in N(cur)
+          if (trial >= (1u << 24) && from_cur) acc = true;
+        }
       } else {
         const gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
         ++trial;
@@ -598,12 +645,13 @@ static int64_t table_budget(gw_graph* g) {
 // edge-centric common-neighbour build; with expected_steps known, build them
 // only when the modelled build time is paid back.
 static bool listed_pays(gw_graph* g, double q) {
+  // the payload answers the lazy has_edge probes of the q < 1 envelope; with
+  // q > 1 k_walk_scale's mixture proposal needs no such probe (and with
+  // q = 1 no probe happens at all), so listed entries are built for q < 1
+  // only, whatever the option says (the walks never depend on options)
+  if (q >= 1.0) return false;
   if (g->opt.listed == 0) return false;
   if (g->opt.listed == 1 || g->opt.expected_steps <= 0) return true;
-  // the payload answers has_edge probes; with q >= 1 the candidates' own
-  // entry reads dominate and listed entries measure no faster (R-MAT-20,
-  // p = 0.25, q = 4: 53.0 vs 52.6 ms per 5.1e8 steps)
-  if (q >= 1.0) return false;
   const double save_s = (double)g->opt.expected_steps * (0.46 / 4.9e10);
   const double build_s = gw_bitset_build_model_s(g);
   if (build_s < 0) {  // the model run failed on the device: keep the plain entries
@@ -970,6 +1018,9 @@ int gw_dev_n2v_walks(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int6
   P.lo = std::min(1.0, P.a_q);
   P.extra = P.a_p > P.M ? P.a_p - P.M : 0.0;
   P.h_prev = std::min(P.a_p, P.M);
+  P.mix_o = std::max(0.0, P.a_p - P.a_q);
+  P.mix_p = 1.0 - P.a_q;
+  P.mix_prev = std::min(1.0, P.a_p / P.a_q);
   P.k0 = (uint32_t)seed;
   P.k1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_STEP;
   P.pk0 = (uint32_t)seed;
@@ -987,15 +1038,16 @@ int gw_dev_n2v_walks(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int6
   hipStream_t s = (hipStream_t)stream;
   const unsigned grid = grid_for(walk_count);
   unsigned long long* C = (unsigned long long*)counters_dev;
-#define GW_LAUNCH(FO, WT, DI)                                                                                      \
+#define GW_LAUNCH_MIX(FO, WT, DI, MX)                                                                              \
   do {                                                                                                             \
     if (g->d.sent)                                                                                                 \
-      k_walk_scale<FO, WT, DI, true><<<grid, kBlock, 0, s>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev, \
-                                                             len_dev, C);                                          \
+      k_walk_scale<FO, WT, DI, true, MX><<<grid, kBlock, 0, s>>>(g->d, P, L, walk_begin, walk_count, shuffle,      \
+                                                                 out_dev, len_dev, C);                             \
     else                                                                                                           \
-      k_walk_scale<FO, WT, DI, false><<<grid, kBlock, 0, s>>>(g->d, P, L, walk_begin, walk_count, shuffle,         \
-                                                              out_dev, len_dev, C);                                \
+      k_walk_scale<FO, WT, DI, false, MX><<<grid, kBlock, 0, s>>>(g->d, P, L, walk_begin, walk_count, shuffle,     \
+                                                                  out_dev, len_dev, C);                            \
   } while (0)
+#define GW_LAUNCH(FO, WT, DI) GW_LAUNCH_MIX(FO, WT, DI, false)
   const bool wt = g->weighted != 0, di = g->directed != 0;
   if (first_order) {
     if (wt) GW_LAUNCH(true, true, false);
@@ -1005,9 +1057,11 @@ int gw_dev_n2v_walks(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int6
     else GW_LAUNCH(false, true, false);
   } else {
     if (di) GW_LAUNCH(false, false, true);
+    else if (P.a_q < 1.0) GW_LAUNCH_MIX(false, false, false, true);  // q > 1: mixture proposal
     else GW_LAUNCH(false, false, false);
   }
 #undef GW_LAUNCH
+#undef GW_LAUNCH_MIX
   GW_HIP_TRY(hipGetLastError());
   return GW_OK;
 }

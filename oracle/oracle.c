@@ -18,7 +18,8 @@
  *     Philox-keyed restatement here is the GPU's parity target and
  *     or_topsim_java (java.util.Random stream) is used statistically.
  *   - or_walks_scale restates the scale-mode sampling design (rejection
- *     sampling of the node2vec.py:61-81 bias); its distribution is checked
+ *     sampling of the node2vec.py:61-81 bias, and for unweighted undirected
+ *     graphs at q > 1 its exact mixture form); its distribution is checked
  *     against exact per-edge probabilities in tests.
  */
 #include <math.h>
@@ -196,6 +197,13 @@ void or_walks_scale(int64_t n, const int64_t* off, const int32_t* nbrs, const do
   const double lo = a_q < 1.0 ? a_q : 1.0;
   const double extra = a_p > M ? a_p - M : 0.0;
   const double h_prev = a_p < M ? a_p : M;
+  /* mixture proposal for unweighted undirected graphs at q > 1 (w = 1/q on
+   * N(cur) + (1 - 1/q) on N(prev) + the return outlier), taken by a step
+   * iff deg(prev) < deg(cur): see k_walk_scale (gw_n2v.hip) */
+  const int mix = !w && !directed && a_q < 1.0;
+  const double mix_o = a_p - a_q > 0.0 ? a_p - a_q : 0.0;
+  const double mix_p = 1.0 - a_q;
+  const double mix_prev = a_p / a_q < 1.0 ? a_p / a_q : 1.0;
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_STEP;
   const uint32_t pk0 = (uint32_t)seed, pk1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_PERM;
   uint64_t tot_steps = 0, tot_trials = 0;
@@ -226,6 +234,36 @@ void or_walks_scale(int64_t n, const int64_t* off, const int32_t* nbrs, const do
         if (w) kk = (gw_u01(u.y) < nq[b + kk]) ? kk : nJ[b + kk];
         slot = b + kk;
         next = nbrs[slot];
+      } else if (mix && off[prev + 1] - off[prev] < d) {
+        const int64_t pb = off[prev], dp = off[prev + 1] - pb;
+        const double Ac = (double)d * a_q;
+        const double H = mix_o + Ac + (double)dp * mix_p;
+        uint32_t trial = 0;
+        for (;;) {
+          struct gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, k0, k1);
+          ++trial;
+          const double r = gw_u01(u.z) * H;
+          if (r < mix_o) { /* return-edge outlier */
+            slot = -1;
+            next = prev;
+            break;
+          }
+          const int from_cur = r < mix_o + Ac;
+          const int64_t s = (from_cur ? b : pb) + (int64_t)gw_index(u.x, u.y, (uint32_t)(from_cur ? d : dp));
+          const int32_t x = nbrs[s];
+          int acc;
+          if (from_cur)
+            acc = x != prev || gw_u01(u.w) < mix_prev;
+          else
+            acc = x != prev && find_slot(off, nbrs, cur, x) >= 0; /* x in N(cur) */
+          if (trial >= (1u << 24) && from_cur) acc = 1;
+          if (acc) {
+            slot = s;
+            next = x;
+            break;
+          }
+        }
+        tot_trials += trial;
       } else {
         const double Wc = w ? wsum[cur] : (double)d;
         const double oa = (back_ok && extra > 0.0) ? extra * w_back : 0.0;

@@ -369,7 +369,7 @@ def test_multichunk_hub_builds_equal_oracle(gw, oracle, tmp_path, mode, p, q):
     inf = G.info()
     assert inf.max_degree > 3 * 4096
     if mode == "rejection":
-        assert inf.listed == 1
+        assert inf.listed == (1 if q < 1 else 0)  # q > 1: the mixture proposal needs no listed entries
     L, begin, count = 30, 123, 6000
     out = torch.empty((count, L), dtype=torch.int32, device="cuda")
     lens = torch.empty(count, dtype=torch.int32, device="cuda")
@@ -512,7 +512,7 @@ def test_rejection_rmat_equals_oracle(gw, oracle, p, q):
 
 
 @pytest.mark.parametrize("graph", ["mixed", "hub"])
-@pytest.mark.parametrize("p,q", [(1, 0.5), (0.25, 4), (4, 0.25)])
+@pytest.mark.parametrize("p,q", [(1, 0.5), (0.25, 0.5), (4, 0.25)])
 def test_rejection_listed_entries_equal_oracle(gw, oracle, tmp_path, graph, p, q):
     """k_walk_listed (REJECTION on an unweighted undirected graph): the lazy
     has_edge(x, prev) test answered from the list / inline / Elias-Fano
@@ -539,6 +539,26 @@ def test_rejection_listed_entries_equal_oracle(gw, oracle, tmp_path, graph, p, q
     np.testing.assert_array_equal(lens.cpu().numpy(), rl)
     assert int(cnt[0]) == int(rc[0]) and int(cnt[1]) == int(rc[1])
     G.free()
+
+
+@pytest.mark.parametrize("listed", [-1, 1])
+def test_no_listed_entries_at_q_ge_1(gw, oracle, listed):
+    """q >= 1: the rejection sampler never builds listed entries, whatever
+    gw_options_t.listed says (q > 1 takes the mixture proposal, which has no
+    lazy has_edge probe for them to answer; q = 1 has no probe at all), so the
+    walks never depend on the option: == oracle.walks_scale."""
+    import torch
+    from gwamd import _lib as C
+    G = gw.GWGraph.rmat(12, 16, 0.57, 0.19, 0.19, 9).to_device(0)
+    G.options(listed=listed)
+    for p, q in [(0.25, 4.0), (2.0, 1.0)]:
+        C.check(C.lib().gw_n2v_prepare(G.handle, p, q, C.N2V_REJECTION), G.handle)
+        assert G.info().listed == 0
+        out = torch.empty((3000, 20), dtype=torch.int32, device="cuda")
+        C.check(C.lib().gw_n2v_walks(G.handle, 20, 4, 100, 3000, 1, C.ptr(out), None, None, None), G.handle)
+        torch.cuda.synchronize()
+        ref, _, _ = oracle.walks_scale(dict(G.export_csr(), weights=None), p, q, 4, 20, 100, 3000, nthreads=4)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
 
 
 def test_native_comm_single_rank_allgather(gw):

@@ -181,20 +181,57 @@ def test_java_format_and_pq(oracle):
     assert [i for i, _ in got] == [2, 1]
 
 
+def _selfloop_csr():
+    """A small undirected simple graph (sorted rows) with self-loops on a
+    third of its vertices, hubs and leaves: both branches of the q > 1 mixture
+    (deg prev < deg cur and not), prev drawn from N(prev) as its own
+    self-loop, and cur's self-loop as a common neighbour."""
+    rng = np.random.default_rng(17)
+    n = 14
+    E = set()
+    for v in range(1, n):
+        E.add((int(rng.integers(0, v)), v))
+    for _ in range(12):
+        a, b = sorted(int(x) for x in rng.integers(0, n, 2))
+        if a != b:
+            E.add((a, b))
+    for v in range(0, n, 3):
+        E.add((v, v))
+    adj = [set() for _ in range(n)]
+    for a, b in E:
+        adj[a].add(b)
+        adj[b].add(a)
+    offs = np.zeros(n + 1, np.int64)
+    offs[1:] = np.cumsum([len(r) for r in adj])
+    nbrs = np.concatenate([np.array(sorted(r), np.int32) for r in adj])
+    return offs, nbrs
+
+
 @pytest.mark.slow
-def test_scale_walks_match_second_order_distribution(oracle):
-    """The rejection design reproduces the reference transition
-    probabilities (alias_edges, node2vec.py:61-81) in distribution."""
-    g = load_golden("n2v_karate_p0.25_q4_s0.npz")
-    rank = {int(x): i for i, x in enumerate(g["labels"])}
-    nbrs = np.array([rank[int(x)] for x in g["nbrs"]], np.int32)
-    offs = g["offsets"]
+@pytest.mark.parametrize("graph", ["karate", "selfloops"])
+@pytest.mark.parametrize("p,q", [(0.25, 4), (4, 2), (0.5, 2), (1, 0.5), (4, 0.25)])
+def test_scale_walks_match_second_order_distribution(oracle, graph, p, q):
+    """The scale sampler reproduces the reference transition probabilities
+    (alias_edges, node2vec.py:61-81) in distribution: the uniform-proposal
+    rejection design (q <= 1) and, at q > 1, the mixture proposal taken when
+    deg(prev) < deg(cur) — including 1/p < 1/q (a prev drawn from N(cur)
+    accepted with probability q/p) and self-loops."""
+    if graph == "karate":
+        g = load_golden("n2v_karate_p0.25_q4_s0.npz")
+        rank = {int(x): i for i, x in enumerate(g["labels"])}
+        nbrs = np.array([rank[int(x)] for x in g["nbrs"]], np.int32)
+        offs = g["offsets"]
+    else:
+        offs, nbrs = _selfloop_csr()
     csr = dict(offsets=offs, nbrs=nbrs, weights=None, node_order=np.arange(len(offs) - 1, dtype=np.int32))
     n = len(offs) - 1
-    out, lens, cnt = oracle.walks_scale(csr, 0.25, 4, seed=3, L=3, walk_begin=0, walk_count=n * 20000,
+    per = 20000 if graph == "karate" else 40000
+    out, lens, cnt = oracle.walks_scale(csr, p, q, seed=3, L=3, walk_begin=0, walk_count=n * per,
                                         nthreads=8)
     # exact P(next | prev, cur) from the reference formula
     counts = {}
+    mixed = 0
+    deg = np.diff(offs)
     for a, b, c in out:
         counts.setdefault((a, b), {}).setdefault(c, 0)
         counts[(a, b)][c] += 1
@@ -203,14 +240,16 @@ def test_scale_walks_match_second_order_distribution(oracle):
         tot = sum(dist.values())
         if tot < 4000:
             continue
+        mixed += int(deg[a] < deg[b])
         row = nbrs[offs[b]:offs[b + 1]]
-        un = np.array([1 / 0.25 if x == a else (1.0 if x in set(nbrs[offs[a]:offs[a + 1]]) else 1 / 4)
-                       for x in row])
+        na = set(nbrs[offs[a]:offs[a + 1]].tolist())
+        un = np.array([1 / p if x == a else (1.0 if x in na else 1 / q) for x in row])
         pr = un / un.sum()
         emp = np.array([dist.get(int(x), 0) for x in row]) / tot
         sd = np.sqrt(pr * (1 - pr) / tot)
         worst = max(worst, float(np.max(np.abs(emp - pr) / np.maximum(sd, 1e-12))))
     assert worst < 5.5, worst
+    assert mixed > 5  # the mixture branch is exercised (taken when deg prev < deg cur)
 
 
 @pytest.mark.slow

@@ -74,11 +74,14 @@ def _max_z(counts, prob_of, min_n):
     ("directed_sinks.edgelist", True, False, " "),
     ("karate.edgelist", False, False, " "),
 ])
-@pytest.mark.parametrize("p,q", [(0.25, 4.0), (4.0, 0.25), (0.5, 2.0)])
+@pytest.mark.parametrize("p,q", [(0.25, 4.0), (4.0, 0.25), (0.5, 2.0), (4.0, 2.0)])
 def test_rejection_walks_follow_reference_law(gw, name, directed, weighted, delim, p, q):
     """k_walk_scale (GW_N2V_REJECTION): weighted rows (node alias proposal),
-    directed rows (has_edge(x, prev) on x's out-row, sinks) and the return-edge
-    outlier envelope (p < 1) against get_alias_edge / alias_nodes."""
+    directed rows (has_edge(x, prev) on x's out-row, sinks), the return-edge
+    outlier envelope (p < 1) and, on the unweighted undirected graph at q > 1,
+    the mixture proposal (steps with deg prev < deg cur; at p = 4, q = 2 a
+    prev drawn from N(cur) is accepted with probability q/p) against
+    get_alias_edge / alias_nodes."""
     from gwamd import _lib as C
     G = gw.GWGraph.from_edgelist(os.path.join(DATA, name), delim, "nx", directed, weighted).to_device(0)
     csr = G.export_csr()
@@ -116,6 +119,44 @@ def test_rejection_walks_follow_reference_law(gw, name, directed, weighted, deli
                 trip[(int(a), int(b))][int(c)] += 1
     z2, used2 = _max_z(trip, lambda ctx: _law(csr, directed, p, q, ctx[0], ctx[1]), 2000)
     assert used2 >= 10 and z2 < 6.0, (z2, used2)
+    G.free()
+
+
+@pytest.mark.parametrize("p,q", [(0.25, 4.0), (4.0, 2.0)])
+def test_mixture_walks_follow_reference_law_selfloops(gw, tmp_path, p, q):
+    """The q > 1 mixture proposal on a graph with self-loops on a third of its
+    vertices, hubs and leaves: prev's own self-loop drawn from N(prev) is
+    rejected, cur's self-loop is a common neighbour (has_edge(cur, prev))."""
+    from gwamd import _lib as C
+    rng = np.random.default_rng(17)
+    n = 14
+    E = set()
+    for v in range(1, n):
+        E.add((int(rng.integers(0, v)), v))
+    for _ in range(12):
+        a, b = sorted(int(x) for x in rng.integers(0, n, 2))
+        if a != b:
+            E.add((a, b))
+    for v in range(0, n, 3):
+        E.add((v, v))
+    path = str(tmp_path / "selfloops.edgelist")
+    with open(path, "w") as f:
+        for a, b in sorted(E):
+            f.write(f"{a} {b}\n")
+    G = gw.GWGraph.from_edgelist(path, " ", "nx").to_device(0)
+    csr = dict(G.export_csr(), weights=None)
+    L = 6
+    W = _walks(gw, G, C.N2V_REJECTION, p, q, L, G.n * 20000, seed=23)
+    deg = np.diff(csr["offsets"])
+    trip = {}
+    mixed = 0
+    for t in range(L - 2):
+        for a, b, c in W[:, t:t + 3]:
+            trip.setdefault((int(a), int(b)), {}).setdefault(int(c), 0)
+            trip[(int(a), int(b))][int(c)] += 1
+    mixed = sum(1 for a, b in trip if deg[a] < deg[b])
+    z2, used2 = _max_z(trip, lambda ctx: _law(csr, False, p, q, ctx[0], ctx[1]), 4000)
+    assert used2 >= 20 and mixed >= 10 and z2 < 6.0, (z2, used2, mixed)
     G.free()
 
 
