@@ -659,6 +659,7 @@ def walk_headline(R, args):
         torch.cuda.synchronize()
         rprep = time.perf_counter() - t0
         launch(first(0), cnt_w, out, None)
+        cnt.zero_()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
@@ -666,8 +667,10 @@ def walk_headline(R, args):
         e1.record(stream)
         torch.cuda.synchronize()
         rw = e0.elapsed_time(e1) * 1e-3
-        alt = end_to_end(rprep, rw, launch_steps, 1.0, "prepare + one step, plain rejection sampler")
+        alt = end_to_end(rprep, rw, launch_steps, 1.0, "prepare + one step, rejection sampler (mixture proposal "
+                                                       "at q > 1, no per-edge tables)")
         alt["walk_steps_per_s"] = launch_steps / rw
+        alt["trials_per_step"] = int(cnt[1].item()) / max(int(cnt[0].item()), 1)
         res["end_to_end_rejection"] = alt
         res["end_to_end_best"] = "bitset" if res["end_to_end"]["total_s"] <= alt["total_s"] else "rejection"
     del out
@@ -794,6 +797,35 @@ def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejectio
     e2e = end_to_end(bprep, sec, bsteps, baseline_r / r_run,
                      f"prepare + {baseline_r} walks from every vertex (BASELINE workload)" +
                      ("" if r_run == baseline_r else f"; the timed launch ran {r_run}, scaled"))
+    e2e_rej = e2e_best = None
+    if bmode == "bitset" and world == 1:
+        # the same BASELINE pass end to end with the rejection sampler (mixture
+        # proposal at q > 1; milliseconds to prepare): a one-shot caller's pick
+        sbytes_b = BG.info().sampler_bytes
+        BG.options(listed=0)
+        t0 = time.perf_counter()
+        C.check(C.lib().gw_n2v_prepare(BG.handle, wp, wq, C.N2V_REJECTION), BG.handle)
+        torch.cuda.synchronize()
+        rprep = time.perf_counter() - t0
+        rout = torch.empty((nb, L), dtype=torch.int32, device=R.dev)
+        rcnt = torch.zeros(2, dtype=torch.int64, device=R.dev)
+        launch(first(1), nb, rout, None)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        launch(first(1), nb, rout, rcnt)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        rw = e0.elapsed_time(e1) * 1e-3
+        rsteps = int(rcnt[0].item())
+        e2e_rej = end_to_end(rprep, rw, rsteps, baseline_r / r_run,
+                             f"prepare + {baseline_r} walks from every vertex, rejection sampler")
+        e2e_rej["walk_steps_per_s"] = rsteps / rw
+        e2e_rej["trials_per_step"] = int(rcnt[1].item()) / max(rsteps, 1)
+        e2e_best = "bitset" if e2e["total_s"] <= e2e_rej["total_s"] else "rejection"
+        del rout
+        BG.options(listed=-1)
+        sbytes = sbytes_b
     return {"metric": f"walk-steps/sec (node2vec, {what})", "value": bsteps / sec, "unit": "walk-steps/s",
             "n_ranks": world, "scaling": "strong" if strong_walks else "weak",
             "config": {"workload": f"node2vec p={wp} q={wq} on Graph500 R-MAT scale-{scale} ef {ef} "
@@ -809,8 +841,9 @@ def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejectio
                          "units_per_launch": local_steps, "pmc_tag": tag,
                          "pmc_match": {"kernel": kname, "grid": grid_threads(nb)},
                          "random_line_roofline": line},
-            "host_build_s": build_s, "prepare_s": bprep, "sampler_tables_gb": BG.info().sampler_bytes / 1e9,
-            "end_to_end": e2e, "allgather": gather, "cpu_baseline": cpu_b}
+            "host_build_s": build_s, "prepare_s": bprep, "sampler_tables_gb": sbytes / 1e9,
+            "end_to_end": e2e, "end_to_end_rejection": e2e_rej, "end_to_end_best": e2e_best,
+            "allgather": gather, "cpu_baseline": cpu_b}
 
 
 TOPSIM_GRAPHS = {"blog": ("blog.txt", 10313, ",", "lshrank blog, V=10313, 333,983 edges"),

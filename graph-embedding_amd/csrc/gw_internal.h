@@ -118,6 +118,11 @@ struct gw_topsim_ws {
   double* acc_row = nullptr;      // [blocks][touch_cap] overflow hash values (hash mode)
   int32_t* ov_keys = nullptr;     // [blocks][touch_cap] overflow hash keys (-1 empty)
   int32_t* touched = nullptr;     // [blocks][touch_cap] claimed overflow slots
+  int pipe = 0;                   // pipelined kernel (levels of the next source built by wave 0 during
+                                  // the walkers): level / spawner scratch doubled per workgroup
+  int64_t enum_cap = 0;           // enumerated-node pair updates per source (pipelined kernel)
+  int32_t* enum_tgt = nullptr;    // [blocks][2][enum_cap]
+  double* enum_val = nullptr;     // [blocks][2][enum_cap]
   unsigned int* src_counter = nullptr;  // work queue head
   int* error_flag = nullptr;      // capacity overflow
 };

@@ -583,6 +583,8 @@ void gw_dev_release(gw_graph* g) {
   dev_free(t.acc_row);
   dev_free(t.ov_keys);
   dev_free(t.touched);
+  dev_free(t.enum_tgt);
+  dev_free(t.enum_val);
   dev_free(t.src_counter);
   dev_free(t.error_flag);
   t = gw_topsim_ws();

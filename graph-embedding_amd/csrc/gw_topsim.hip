@@ -74,6 +74,9 @@ struct TsArgs {
   double* spawn_mass;
   int32_t* ov_keys;
   double* ov_vals;
+  int32_t* enum_tgt;  // pipelined kernel: enumerated-node pair updates of a source, [blocks][2][enum_cap]
+  double* enum_val;
+  int64_t enum_cap;
   int32_t* touched;
   unsigned int* src_counter;
   int* error_flag;
@@ -188,9 +191,28 @@ struct TsHash {
   __device__ static __forceinline__ uint32_t next(uint32_t h) { return h + 1 == (uint32_t)SLOTS ? 0u : h + 1; }
 };
 
-template <int STEP, int MODE, int BLOCK = TS_BLOCK>
+// per-buffer state of the pipelined kernel (PIPE): the source whose levels
+// wave 0 built into that buffer
+struct TsPipeMeta {
+  long long r;  // index into A.sources
+  int s, ds;
+  int nspawn, nwalk, ncontrib;
+  int valid;
+};
+
+// PIPE (TopSim_singleSample, hash accumulator): the deterministic levels of
+// source s+1 are built by wave 0 alone (wave scans and lane shuffles, no
+// workgroup barrier) into the second half of double-buffered level /
+// spawner scratch while the other waves run the walkers of source s; wave 0
+// then joins them.  Walkers and the enumerated nodes' pair updates (wave 0
+// records them as (target, value) lists instead of adding them while the
+// accumulator belongs to source s) are dealt out 64 at a time from an LDS
+// counter, so the workgroup's barrier-bound level phase (28% of its cycles
+// at P10M) overlaps its walkers instead of stalling every wave.
+template <int STEP, int MODE, int BLOCK = TS_BLOCK, bool PIPE = false>
 __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   constexpr int NW = BLOCK / 64;
+  constexpr int NB = PIPE ? 2 : 1;  // level / spawner scratch buffers per workgroup
   constexpr int CO_LDS = TS_CO_LDS;
   constexpr bool LDS_ROW = MODE == 0;
   using H = TsHash<MODE>;
@@ -226,16 +248,21 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   const gw_dev_graph& G = A.G;
   const int n = (int)G.n;
   const int64_t cap = A.level_cap;
-  int32_t* V = A.lvl_vertex + blk * (int64_t)(L + 1) * cap;
-  int32_t* P = A.lvl_parent + blk * (int64_t)(L + 1) * cap;
-  int32_t* D = A.lvl_deg + blk * (int64_t)(L + 1) * cap;
-  int64_t* O = A.lvl_off + blk * (int64_t)(L + 1) * cap;
+  // level / spawner scratch of buffer b (PIPE: two, the source being walked
+  // and the next one; otherwise one)
+  const int64_t lvl_stride = (int64_t)(L + 1) * cap;
+  int32_t* V = A.lvl_vertex + blk * NB * lvl_stride;
+  int32_t* P = A.lvl_parent + blk * NB * lvl_stride;
+  int32_t* D = A.lvl_deg + blk * NB * lvl_stride;
+  int64_t* O = A.lvl_off + blk * NB * lvl_stride;
   double* M = A.lvl_mass + blk * 2 * cap;
   int32_t* CO = A.child_off + blk * (cap + 1);
-  int32_t* SN = A.spawn_node + blk * A.spawn_cap;
-  int32_t* SL = A.spawn_level + blk * A.spawn_cap;
-  int32_t* SF = A.spawn_first + blk * (A.spawn_cap + 1);
-  double* SM = A.spawn_mass + blk * A.spawn_cap;
+  int32_t* SN = A.spawn_node + blk * NB * A.spawn_cap;
+  int32_t* SL = A.spawn_level + blk * NB * A.spawn_cap;
+  int32_t* SF = A.spawn_first + blk * NB * (A.spawn_cap + 1);
+  double* SM = A.spawn_mass + blk * NB * A.spawn_cap;
+  __shared__ TsPipeMeta s_pm[2];
+  __shared__ unsigned s_wnext;
   // accumulator: dense LDS row (small n) or LDS open-addressing hash with a
   // per-workgroup HBM overflow hash (large n)
   double* s_hval = s_row;                                   // [HASH_SLOTS]
@@ -329,6 +356,185 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     ++my_upd;
   };
 
+  // ---- PIPE: wave 0 builds the levels of sources[r] into buffer b ---------
+  // Same queue order, records and pair updates as the workgroup version in
+  // the source loop below; control flow is wave-uniform, lanes exchange
+  // through shuffles (child -> parent by a binary search over the chunk's
+  // inclusive child counts held one per lane), and the wave's own global
+  // writes are fenced before it reads them back.
+  auto wave_levels = [&](int b, int64_t r) {
+    const int lane = tid & 63;
+    int32_t* Vb = V + b * lvl_stride;
+    int32_t* Pb = P + b * lvl_stride;
+    int32_t* Db = D + b * lvl_stride;
+    int64_t* Ob = O + b * lvl_stride;
+    int32_t* SNb = SN + b * A.spawn_cap;
+    int32_t* SLb = SL + b * A.spawn_cap;
+    int32_t* SFb = SF + b * (A.spawn_cap + 1);
+    double* SMb = SM + b * A.spawn_cap;
+    int32_t* ETb = A.enum_tgt + (blk * 2 + b) * A.enum_cap;
+    double* EVb = A.enum_val + (blk * 2 + b) * A.enum_cap;
+    const int32_t s = A.sources[r];
+    const int ds = G.deg[s];
+    if (lane == 0) {
+      Vb[0] = s;
+      Db[0] = ds;
+      Ob[0] = G.offsets[s];
+      Pb[0] = -1;
+      M[0] = A.sampled;  // path[0].sample = SAMPLE (:73)
+    }
+    __threadfence_block();
+    int sz = 1, nsp = 0, nwk = 0, nct = 0;
+    bool abort = false;
+    for (int l = 0; l <= L && sz > 0; ++l) {
+      if (lane == 0 && sz > my_maxf) my_maxf = sz;
+      const double* Ml = M + (int64_t)(l & 1) * cap;
+      if ((l & 1) == 0 && l >= 2) {  // computePathSim at pathLen = 2i (:80-83, :157): recorded
+        for (int j0 = 0; j0 < sz; j0 += 64) {
+          const int j = j0 + lane;
+          int32_t tgt = -1;
+          double val = 0.0;
+          if (j < sz) {
+            int32_t path[L + 1], dpath[L + 1];
+            int p = j;
+#pragma unroll
+            for (int t = L; t >= 1; --t) {
+              if (t <= l) {
+                path[t] = Vb[(int64_t)t * cap + p];
+                dpath[t] = Db[(int64_t)t * cap + p];
+                p = Pb[(int64_t)t * cap + p];
+              }
+            }
+            path[0] = s;
+            dpath[0] = ds;
+#pragma unroll
+            for (int t = 2; t <= L; t += 2) {
+              if (t == l) {
+                const int i = t / 2;
+                bool meet = path[t] != s;  // :183
+#pragma unroll
+                for (int q = 0; q < STEP; ++q)  // isFirstMeet (:211-218)
+                  if (q < i && path[q] == path[t - q]) meet = false;
+                if (meet) {
+                  tgt = path[t];
+                  val = ((Ml[j] * A.cache[i]) * (double)dpath[i]) / (double)dpath[t];  // :189
+                  ++my_upd;
+                }
+              }
+            }
+          }
+          const unsigned long long em = __ballot(tgt >= 0);
+          const int k = nct + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+          if (tgt >= 0 && k < A.enum_cap) {
+            ETb[k] = tgt;
+            EVb[k] = val;
+          }
+          nct += __popcll(em);
+        }
+        if (nct > A.enum_cap) abort = true;
+      }
+      if (l == L || abort) break;
+      int32_t* Vn = Vb + (int64_t)(l + 1) * cap;
+      int32_t* Pn = Pb + (int64_t)(l + 1) * cap;
+      int32_t* Dn = Db + (int64_t)(l + 1) * cap;
+      int64_t* On = Ob + (int64_t)(l + 1) * cap;
+      double* Mn = M + (int64_t)((l + 1) & 1) * cap;
+      const int32_t* Dl = Db + (int64_t)l * cap;
+      const int64_t* Ol = Ob + (int64_t)l * cap;
+      int tot = 0;
+      for (int j0 = 0; j0 < sz; j0 += 64) {
+        const int j = j0 + lane;
+        int cnt = 0, c = 0, d = 0;
+        double m = 0.0;
+        int64_t o = 0;
+        if (j < sz) {
+          d = Dl[j];
+          m = Ml[j];
+          o = Ol[j];
+          if (d != 0 && m >= (double)d) {  // enumerate (:99)
+            cnt = d;
+          } else if (d != 0) {  // d == 0: randNeighbor() == -1 -> no child (:143-144)
+            c = (int)m;         // number = (int)s == s ? (int)s : (int)s + 1 (:131-135)
+            if ((double)c != m) c += 1;
+          }
+        }
+        int ic = cnt, iw = c;  // inclusive wave scans: children, walkers
+#pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+          const int a = __shfl_up(ic, dd, 64), w = __shfl_up(iw, dd, 64);
+          if (lane >= dd) {
+            ic += a;
+            iw += w;
+          }
+        }
+        const int ctot = __shfl(ic, 63, 64), wtot = __shfl(iw, 63, 64);
+        const unsigned long long spm = __ballot(c > 0);
+        const int ksp = nsp + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(spm >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)spm, 0u));
+        if (c > 0 && ksp < A.spawn_cap) {
+          SLb[ksp] = l;
+          SNb[ksp] = j;
+          SFb[ksp] = nwk + iw - c;        // first walker of this spawner (queue order)
+          SMb[ksp] = m / (double)c;      // (double)cur.sample/(double)number (:142)
+        }
+        nsp += __popcll(spm);
+        nwk += wtot;
+        if (nsp > A.spawn_cap || (int64_t)tot + ctot > cap) {
+          abort = true;
+          break;
+        }
+        // the chunk's children, BFS queue order (edges.get(k), insertion order :103-110)
+        for (int c0 = 0; c0 < ctot; c0 += 64) {
+          const int cc = c0 + lane;
+          int pl = 0;  // parent lane: the first lane whose inclusive count exceeds cc
+#pragma unroll
+          for (int st = 32; st >= 1; st >>= 1)
+            if (__shfl(ic, pl + st - 1, 64) <= cc) pl += st;
+          const int pd = __shfl(cnt, pl, 64);
+          const int pex = __shfl(ic, pl, 64) - pd;
+          const int64_t po = ((int64_t)__shfl((int)(o >> 32), pl, 64) << 32) | (uint32_t)__shfl((int)o, pl, 64);
+          const double pm = __shfl(m, pl, 64);
+          if (cc < ctot) {
+            const gw_ts_ent e = gw_ts_load(A.ent + po + (cc - pex));
+            const int ci = tot + cc;
+            Vn[ci] = e.x;
+            Dn[ci] = e.d;
+            On[ci] = e.off;
+            Pn[ci] = j0 + pl;
+            Mn[ci] = pm / (double)pd;  // newSample = cur.sample / degree (:104)
+          }
+        }
+        tot += ctot;
+      }
+      if (abort) break;
+      if (lane == 0) my_ext += tot;
+      sz = tot;
+      __threadfence_block();
+    }
+    if (abort && lane == 0) atomicOr(A.error_flag, 1);
+    if (lane == 0) {
+      SFb[abort ? 0 : nsp] = abort ? 0 : nwk;
+      s_pm[b].r = r;
+      s_pm[b].s = s;
+      s_pm[b].ds = ds;
+      s_pm[b].nspawn = abort ? 0 : nsp;
+      s_pm[b].nwalk = abort ? 0 : nwk;
+      s_pm[b].ncontrib = abort ? 0 : min(nct, (int)A.enum_cap);
+      s_pm[b].valid = 1;
+    }
+  };
+  // PIPE: wave 0 claims the next source and builds its levels into buffer b
+  auto claim_and_build = [&](int b) {
+    long long r = 0;
+    if (tid == 0) r = (long long)atomicAdd(A.src_counter, 1u);
+    r = ((long long)__shfl((int)(r >> 32), 0, 64) << 32) | (uint32_t)__shfl((int)r, 0, 64);
+    if (r < A.nsrc)
+      wave_levels(b, (int64_t)r);
+    else if (tid == 0)
+      s_pm[b].valid = 0;
+  };
+
   __shared__ unsigned long long s_ph[11];  // diagnostics only: [10] = last timestamp
   if (tid == 0)
     for (int k = 0; k < 11; ++k) s_ph[k] = 0;
@@ -339,18 +545,107 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       s_ph[10] = now;
     }
   };
+  // one walker (index g in the reference's BFS queue order) of source s from
+  // the level / spawner records of buffer b
+  auto run_walker = [&](int g, int b, int32_t s, int ds, int ns) {
+    const int32_t* Vb = V + b * lvl_stride;
+    const int32_t* Db = D + b * lvl_stride;
+    const int32_t* Pb = P + b * lvl_stride;
+    const int64_t* Ob = O + b * lvl_stride;
+    const int32_t* SFb = SF + b * (A.spawn_cap + 1);
+    const int sp = upper_bound_i32(ns + 1 <= CO_LDS ? s_co : SFb, ns + 1, g) - 1;
+    const int l0 = SL[b * A.spawn_cap + sp];
+    const double mw = SM[b * A.spawn_cap + sp];
+    int32_t path[L + 1], dpath[L + 1];
+    int p = SN[b * A.spawn_cap + sp];
+    int32_t dcur = ds;
+    int64_t ocur = rw ? G.offsets[s] : (l0 == 0 ? Ob[0] : Ob[(int64_t)l0 * cap + p]);
+#pragma unroll
+    for (int t = L; t >= 1; --t) {
+      if (t <= l0) {
+        path[t] = Vb[(int64_t)t * cap + p];
+        dpath[t] = Db[(int64_t)t * cap + p];
+        p = Pb[(int64_t)t * cap + p];
+      }
+    }
+    path[0] = s;
+    dpath[0] = ds;
+#pragma unroll
+    for (int t = 0; t <= L; ++t)
+      if (t == l0) dcur = dpath[t];
+    bool alive = true;
+#pragma unroll
+    for (int t = 1; t <= L; ++t) {
+      if (t > l0 && alive) {
+        if (dcur == 0) {
+          alive = false;
+        } else {
+          uint32_t ux, uy = 0u;
+          if (kGwDiag && (A.diag & 2)) {
+            ux = ((uint32_t)s * 0x9E3779B1u) ^ ((uint32_t)g * 0x85EBCA6Bu) ^ ((uint32_t)t * 0xC2B2AE35u);
+            ux ^= ux >> 15;
+            ux *= 0x2C1B3C6Du;
+          } else {
+            const gw_u4 u = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)t, 0u, A.k0, A.k1);
+            ux = u.x;
+            uy = u.y;
+          }
+          uint64_t ei = (uint64_t)ocur + gw_index(ux, uy, (uint32_t)dcur);
+          if (kGwDiag && (A.diag & 12))  // timing only: walker reads confined to 1 GB / 2 GB of the table
+            ei &= (A.diag & 4) ? ((1ull << 26) - 1) : ((1ull << 27) - 1);
+          const gw_ts_ent e = gw_ts_load(A.ent + ei);  // randNeighbor
+          path[t] = e.x;
+          dpath[t] = e.d;
+          dcur = e.d;
+          ocur = e.off;
+          ++my_ext;
+          if ((t & 1) == 0 && !(kGwDiag && (A.diag & 1))) contrib(path, dpath, t / 2, s, mw);
+        }
+      }
+    }
+    ++my_walk;
+  };
+
+  int cur = 0;  // PIPE: buffer of the source being walked
+  if (PIPE) {
+    if (tid < 64) claim_and_build(0);
+    __syncthreads();
+  }
   for (;;) {
     mark(-1);
+    int64_t r;
+    int32_t s;
+    int ds;
+    int p_ns = 0, p_nw = 0, p_ne = 0;
+    if (PIPE) {
+      // hand-over: the source whose levels wave 0 built during the last walker phase
+      if (!s_pm[cur].valid) break;
+      r = s_pm[cur].r;
+      s = s_pm[cur].s;
+      ds = s_pm[cur].ds;
+      p_ns = s_pm[cur].nspawn;
+      p_nw = s_pm[cur].nwalk;
+      p_ne = s_pm[cur].ncontrib;
+      if (p_ns + 1 <= CO_LDS) {
+        const int32_t* SFb = SF + cur * (A.spawn_cap + 1);
+        for (int k = tid; k <= p_ns; k += BLOCK) s_co[k] = SFb[k];
+      }
+      if (tid == 0) {
+        s_wnext = 0u;
+        s_ncomp = 0;
+      }
+      __syncthreads();
+    } else {
     if (tid == 0) {
       s_src = (int)atomicAdd(A.src_counter, 1u);
       s_abort = 0;
       s_ncomp = 0;
     }
     __syncthreads();
-    const int64_t r = s_src;
+    r = s_src;
     if (r >= A.nsrc) break;
-    const int32_t s = A.sources[r];
-    const int ds = G.deg[s];
+    s = A.sources[r];
+    ds = G.deg[s];
 
     if (rw) {
       if (tid == 0) {
@@ -499,64 +794,33 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       __syncthreads();
     }
 
+    }  // !PIPE: levels built by the whole workgroup
+
     mark(1);
     // random walkers: one lane each, path in registers
-    {
+    if (PIPE) {
+      // wave 0 first builds the next source's levels into the other buffer
+      if (tid < 64) claim_and_build(cur ^ 1);
+      // walkers g < p_nw, then the enumerated nodes' recorded pair updates,
+      // dealt out 64 at a time
+      const int lane = tid & 63;
+      const int32_t* ETb = A.enum_tgt + (blk * 2 + cur) * A.enum_cap;
+      const double* EVb = A.enum_val + (blk * 2 + cur) * A.enum_cap;
+      for (;;) {
+        unsigned base = 0u;
+        if (lane == 0) base = atomicAdd(&s_wnext, 64u);
+        base = (unsigned)__shfl((int)base, 0, 64);
+        if ((int)base >= p_nw + p_ne) break;
+        const int g = (int)base + lane;
+        if (g < p_nw)
+          run_walker(g, cur, s, ds, p_ns);
+        else if (g < p_nw + p_ne)
+          add(ETb[g - p_nw], EVb[g - p_nw]);
+      }
+    } else {
       const int W = s_nwalk;
       const int ns = s_nspawn;
-      for (int g = tid; g < W; g += BLOCK) {
-        const int sp = upper_bound_i32(ns + 1 <= CO_LDS ? s_co : SF, ns + 1, g) - 1;
-        const int l0 = SL[sp];
-        const double mw = SM[sp];
-        int32_t path[L + 1], dpath[L + 1];
-        int p = SN[sp];
-        int32_t dcur = ds;
-        int64_t ocur = rw ? G.offsets[s] : (l0 == 0 ? O[0] : O[(int64_t)l0 * cap + p]);
-#pragma unroll
-        for (int t = L; t >= 1; --t) {
-          if (t <= l0) {
-            path[t] = V[(int64_t)t * cap + p];
-            dpath[t] = D[(int64_t)t * cap + p];
-            p = P[(int64_t)t * cap + p];
-          }
-        }
-        path[0] = s;
-        dpath[0] = ds;
-#pragma unroll
-        for (int t = 0; t <= L; ++t)
-          if (t == l0) dcur = dpath[t];
-        bool alive = true;
-#pragma unroll
-        for (int t = 1; t <= L; ++t) {
-          if (t > l0 && alive) {
-            if (dcur == 0) {
-              alive = false;
-            } else {
-              uint32_t ux, uy = 0u;
-              if (kGwDiag && (A.diag & 2)) {
-                ux = ((uint32_t)s * 0x9E3779B1u) ^ ((uint32_t)g * 0x85EBCA6Bu) ^ ((uint32_t)t * 0xC2B2AE35u);
-                ux ^= ux >> 15;
-                ux *= 0x2C1B3C6Du;
-              } else {
-                const gw_u4 u = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)t, 0u, A.k0, A.k1);
-                ux = u.x;
-                uy = u.y;
-              }
-              uint64_t ei = (uint64_t)ocur + gw_index(ux, uy, (uint32_t)dcur);
-              if (kGwDiag && (A.diag & 12))  // timing only: walker reads confined to 1 GB / 2 GB of the table
-                ei &= (A.diag & 4) ? ((1ull << 26) - 1) : ((1ull << 27) - 1);
-              const gw_ts_ent e = gw_ts_load(A.ent + ei);  // randNeighbor
-              path[t] = e.x;
-              dpath[t] = e.d;
-              dcur = e.d;
-              ocur = e.off;
-              ++my_ext;
-              if ((t & 1) == 0 && !(kGwDiag && (A.diag & 1))) contrib(path, dpath, t / 2, s, mw);
-            }
-          }
-        }
-        ++my_walk;
-      }
+      for (int g = tid; g < W; g += BLOCK) run_walker(g, 0, s, ds, ns);
     }
     __syncthreads();
 
@@ -873,6 +1137,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     }
     __syncthreads();
     mark(4);
+    if (PIPE) cur ^= 1;
   }
 
   if (kGwDiag && A.phase && tid == 0)
@@ -897,6 +1162,12 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim(TsArgs A) {
 template <int STEP, int MODE>
 __global__ void __launch_bounds__(TS_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) k_topsim_2wg(TsArgs A) {
   topsim_body<STEP, MODE>(A);
+}
+
+// pipelined TopSim_singleSample (hash accumulator, two workgroups per CU)
+template <int STEP>
+__global__ void __launch_bounds__(TS_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) k_topsim_pipe(TsArgs A) {
+  topsim_body<STEP, 2, TS_BLOCK, true>(A);
 }
 
 template <typename T>
@@ -944,22 +1215,29 @@ hipError_t launch_step(const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
 }
 
 template <int STEP>
-hipError_t launch_mode(int mode, const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
+hipError_t launch_mode(int mode, bool pipe, const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
+  if (mode == 2 && pipe) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_topsim_pipe<STEP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    k_topsim_pipe<STEP><<<blocks, TS_BLOCK, lds, s>>>(A);
+    return hipGetLastError();
+  }
   if (mode == 2) return launch_step<STEP, 2, true>(A, blocks, lds, s);
   if (mode == 1) return launch_step<STEP, 1, false>(A, blocks, lds, s);
   return lds <= TS_2WG_LDS ? launch_step<STEP, 0, true>(A, blocks, lds, s) : launch_step<STEP, 0, false>(A, blocks, lds, s);
 }
 
-hipError_t launch(int step, int mode, const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
+hipError_t launch(int step, int mode, bool pipe, const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
   switch (step) {
-    case 1: return launch_mode<1>(mode, A, blocks, lds, s);
-    case 2: return launch_mode<2>(mode, A, blocks, lds, s);
-    case 3: return launch_mode<3>(mode, A, blocks, lds, s);
-    case 4: return launch_mode<4>(mode, A, blocks, lds, s);
-    case 5: return launch_mode<5>(mode, A, blocks, lds, s);
-    case 6: return launch_mode<6>(mode, A, blocks, lds, s);
-    case 7: return launch_mode<7>(mode, A, blocks, lds, s);
-    case 8: return launch_mode<8>(mode, A, blocks, lds, s);
+    case 1: return launch_mode<1>(mode, pipe, A, blocks, lds, s);
+    case 2: return launch_mode<2>(mode, pipe, A, blocks, lds, s);
+    case 3: return launch_mode<3>(mode, pipe, A, blocks, lds, s);
+    case 4: return launch_mode<4>(mode, pipe, A, blocks, lds, s);
+    case 5: return launch_mode<5>(mode, pipe, A, blocks, lds, s);
+    case 6: return launch_mode<6>(mode, pipe, A, blocks, lds, s);
+    case 7: return launch_mode<7>(mode, pipe, A, blocks, lds, s);
+    case 8: return launch_mode<8>(mode, pipe, A, blocks, lds, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -998,6 +1276,8 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   ws_free(t.acc_row);
   ws_free(t.ov_keys);
   ws_free(t.touched);
+  ws_free(t.enum_tgt);
+  ws_free(t.enum_val);
   ws_free(t.src_counter);
   ws_free(t.error_flag);
   const int64_t n = g->n;
@@ -1033,8 +1313,16 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
     touch_cap = 1;
     while (touch_cap < want) touch_cap <<= 1;
   }
-  const int64_t per_block = (int64_t)(L + 1) * level_cap * 20 + 2 * level_cap * 8 + (level_cap + 1) * 4 +
-                            spawn_cap * 20 + 4 + (lds_row ? 0 : touch_cap * 16);
+  // TopSim_singleSample with the hash accumulator runs pipelined (k_topsim_pipe):
+  // two level / spawner buffers per workgroup plus the enumerated nodes'
+  // recorded pair updates (<= STEP even levels of level_cap nodes)
+  bool pipe = variant == GW_TOPSIM_SINGLE_SAMPLE && mode == 2;
+  if (const char* np = GW_DIAG_ENV("GW_DIAG_TS_NOPIPE"))  // A/B knob: the unpipelined kernel
+    if (np[0] == '1') pipe = false;
+  const int64_t nb = pipe ? 2 : 1;
+  const int64_t enum_cap = pipe ? (int64_t)step * level_cap : 1;
+  const int64_t per_block = nb * ((int64_t)(L + 1) * level_cap * 20 + spawn_cap * 20 + 4) + 2 * level_cap * 8 +
+                            (level_cap + 1) * 4 + (pipe ? 2 * enum_cap * 12 : 0) + (lds_row ? 0 : touch_cap * 16);
   int dev_cus = 256;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, g->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
@@ -1046,16 +1334,18 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
     return GW_ERR_CAPACITY;
   }
   int rc;
-  if ((rc = ws_alloc(g, &t.lvl_vertex, blocks * (L + 1) * level_cap)) ||
-      (rc = ws_alloc(g, &t.lvl_parent, blocks * (L + 1) * level_cap)) ||
-      (rc = ws_alloc(g, &t.lvl_deg, blocks * (L + 1) * level_cap)) ||
-      (rc = ws_alloc(g, &t.lvl_off, blocks * (L + 1) * level_cap)) ||
+  if ((rc = ws_alloc(g, &t.lvl_vertex, blocks * nb * (L + 1) * level_cap)) ||
+      (rc = ws_alloc(g, &t.lvl_parent, blocks * nb * (L + 1) * level_cap)) ||
+      (rc = ws_alloc(g, &t.lvl_deg, blocks * nb * (L + 1) * level_cap)) ||
+      (rc = ws_alloc(g, &t.lvl_off, blocks * nb * (L + 1) * level_cap)) ||
       (rc = ws_alloc(g, &t.lvl_mass, blocks * 2 * level_cap)) ||
       (rc = ws_alloc(g, &t.child_off, blocks * (level_cap + 1))) ||
-      (rc = ws_alloc(g, &t.spawn_node, blocks * spawn_cap)) ||
-      (rc = ws_alloc(g, &t.spawn_level, blocks * spawn_cap)) ||
-      (rc = ws_alloc(g, &t.spawn_first, blocks * (spawn_cap + 1))) ||
-      (rc = ws_alloc(g, &t.spawn_mass, blocks * spawn_cap)) ||
+      (rc = ws_alloc(g, &t.spawn_node, blocks * nb * spawn_cap)) ||
+      (rc = ws_alloc(g, &t.spawn_level, blocks * nb * spawn_cap)) ||
+      (rc = ws_alloc(g, &t.spawn_first, blocks * nb * (spawn_cap + 1))) ||
+      (rc = ws_alloc(g, &t.spawn_mass, blocks * nb * spawn_cap)) ||
+      (rc = ws_alloc(g, &t.enum_tgt, blocks * 2 * enum_cap)) ||
+      (rc = ws_alloc(g, &t.enum_val, blocks * 2 * enum_cap)) ||
       (rc = ws_alloc(g, &t.touched, blocks * touch_cap)) ||
       (rc = ws_alloc(g, &t.src_counter, 1)) || (rc = ws_alloc(g, &t.error_flag, 1)))
     return rc;
@@ -1079,6 +1369,8 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   t.spawn_cap = spawn_cap;
   t.touch_cap = touch_cap;
   t.lds_row = mode;
+  t.pipe = pipe ? 1 : 0;
+  t.enum_cap = enum_cap;
   t.lds_bytes = lds_row ? (size_t)n * 8 : (size_t)(mode == 2 ? TsHash<2>::SLOTS : TsHash<1>::SLOTS) * 12;
   GW_HIP_TRY(hipDeviceSynchronize());
   return GW_OK;
@@ -1134,6 +1426,9 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   A.spawn_mass = t.spawn_mass;
   A.ov_keys = t.ov_keys;
   A.ov_vals = t.acc_row;
+  A.enum_tgt = t.enum_tgt;
+  A.enum_val = t.enum_val;
+  A.enum_cap = t.enum_cap;
   A.touched = t.touched;
   A.src_counter = t.src_counter;
   A.error_flag = t.error_flag;
@@ -1147,7 +1442,7 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
     GW_HIP_TRY(hipMalloc((void**)&A.phase, 10 * sizeof(unsigned long long)));
     GW_HIP_TRY(hipMemsetAsync(A.phase, 0, 10 * sizeof(unsigned long long), s));
   }
-  hipError_t e = launch(step, t.lds_row, A, blocks, t.lds_bytes, s);
+  hipError_t e = launch(step, t.lds_row, t.pipe != 0, A, blocks, t.lds_bytes, s);
   if (e != hipSuccess) {
     g->err = std::string("k_topsim launch: ") + hipGetErrorString(e);
     return GW_ERR_DEVICE;
