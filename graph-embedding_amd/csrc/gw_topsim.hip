@@ -42,6 +42,7 @@ constexpr int TS_WAVES = TS_BLOCK / 64;
 constexpr int TOPK_MAX = 256;
 constexpr int TS_CO_LDS = 1792;  // child / spawner offsets kept in LDS up to this many entries
 constexpr int64_t LDS_ROW_MAX_BYTES = 96 * 1024;
+constexpr int kPipeMaxSample = 2048;  // k_topsim_pipe for SAMPLE up to this
 
 struct TsArgs {
   gw_dev_graph G;
@@ -1316,7 +1317,11 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   // TopSim_singleSample with the hash accumulator runs pipelined (k_topsim_pipe):
   // two level / spawner buffers per workgroup plus the enumerated nodes'
   // recorded pair updates (<= STEP even levels of level_cap nodes)
-  bool pipe = variant == GW_TOPSIM_SINGLE_SAMPLE && mode == 2;
+  // (wave 0 alone expands the enumerated levels: worth it while they are
+  // small next to the walkers — P10M, SAMPLE 1000: ~130 enumerated nodes and
+  // ~1,060 walkers per source — not for SAMPLE in the thousands on low-degree
+  // graphs, whose levels reach thousands of nodes)
+  bool pipe = variant == GW_TOPSIM_SINGLE_SAMPLE && mode == 2 && sample <= kPipeMaxSample;
   if (const char* np = GW_DIAG_ENV("GW_DIAG_TS_NOPIPE"))  // A/B knob: the unpipelined kernel
     if (np[0] == '1') pipe = false;
   const int64_t nb = pipe ? 2 : 1;
