@@ -52,10 +52,13 @@ def test_topsim_dense_equals_oracle(gw, oracle, name, sample, step):
     assert st[0] == rst["extensions"] and st[1] == rst["pair_updates"] and st[3] == rst["walkers"]
 
 
-@pytest.mark.parametrize("sample,stride", [(5000, 97), (40000, 1931)])
+@pytest.mark.parametrize("sample,stride", [(5000, 97), (40000, 1931), (1000, 53), (2000, 211)])
 def test_topsim_large_n_hash_accumulator(gw, oracle, sample, stride):
     """arxiv (n=38741 > LDS row) takes the LDS-hash path (overflow into the
-    HBM hash is exercised by test_topsim_hash_overflow_rmat)."""
+    HBM hash is exercised by test_topsim_hash_overflow_rmat); SAMPLE <= 2048
+    runs the pipelined kernel (wave 0 builds the next source's levels while
+    the other waves walk): same rows, and the same extension / pair-update /
+    walker counts as the reference's queue."""
     g = _graph(gw, "arxiv")
     sources = np.arange(0, 38741, stride, dtype=np.int32)
     rows, st = _dense_gpu(g, 0, sample, 5, sources)
@@ -63,6 +66,7 @@ def test_topsim_large_n_hash_accumulator(gw, oracle, sample, stride):
     np.testing.assert_allclose(rows, ref, rtol=1e-12, atol=1e-9)
     assert np.array_equal(rows > 0, ref > 0)
     assert st[1] == rst["pair_updates"]
+    assert st[0] == rst["extensions"] and st[3] == rst["walkers"]
 
 
 @pytest.mark.parametrize("step", [1, 2])
@@ -169,9 +173,11 @@ def test_cpp_driver_matches_oracle(gw, oracle, tmp_path):
         assert got[v].decode() == f"{v}" + "".join(f"\t{i}:{oracle.java_format_fixed(x)}" for i, x in exp)
 
 
-def test_topsim_hash_overflow_rmat(gw, oracle):
+@pytest.mark.parametrize("sample,step", [(20000, 3), (2000, 4)])
+def test_topsim_hash_overflow_rmat(gw, oracle, sample, step):
     """Hub sources of a Java-semantics R-MAT-15 graph reach > 6144 distinct
-    targets: the LDS hash overflows into the HBM hash, results unchanged."""
+    targets: the LDS hash overflows into the HBM hash, results unchanged
+    (SAMPLE 2000: the pipelined kernel)."""
     import torch
     from gwamd import _lib as Cl
     G = gw.GWGraph.rmat(15, 8, seed=3)
@@ -183,12 +189,12 @@ def test_topsim_hash_overflow_rmat(gw, oracle):
     jc = J.export_csr()
     J.to_device(0)
     top = np.argsort(-np.diff(jc["offsets"]))[:16].astype(np.int32)
-    ref, rst = oracle.topsim(jc["offsets"], jc["nbrs"], 0, 20000, 3, seed=9, sources=top, nthreads=8)
-    assert (ref > 0).sum(axis=1).max() > 6144
+    ref, rst = oracle.topsim(jc["offsets"], jc["nbrs"], 0, sample, step, seed=9, sources=top, nthreads=8)
+    assert (ref > 0).sum(axis=1).max() > 4608  # past the 6144-slot LDS hash's load limit
     src = torch.as_tensor(top, device="cuda")
     out = torch.empty((len(top), len(deg)), dtype=torch.float64, device="cuda")
     st = torch.zeros(4, dtype=torch.int64, device="cuda")
-    Cl.check(Cl.lib().gw_topsim_dense(J.handle, 0, 20000, 3, 0.6, 9, Cl.ptr(src), len(top), Cl.ptr(out),
+    Cl.check(Cl.lib().gw_topsim_dense(J.handle, 0, sample, step, 0.6, 9, Cl.ptr(src), len(top), Cl.ptr(out),
                                       Cl.ptr(st), None), J.handle)
     np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-12, atol=1e-9)
     assert int(st[1]) == rst["pair_updates"]
@@ -196,7 +202,7 @@ def test_topsim_hash_overflow_rmat(gw, oracle):
     k = 100
     ids = torch.empty((len(top), k), dtype=torch.int32, device="cuda")
     sc = torch.empty((len(top), k), dtype=torch.float64, device="cuda")
-    Cl.check(Cl.lib().gw_topsim(J.handle, 0, 20000, 3, 0.6, 9, Cl.ptr(src), len(top), k, Cl.ptr(ids), Cl.ptr(sc),
+    Cl.check(Cl.lib().gw_topsim(J.handle, 0, sample, step, 0.6, 9, Cl.ptr(src), len(top), k, Cl.ptr(ids), Cl.ptr(sc),
                                 None, None), J.handle)
     for r in range(len(top)):
         row = ref[r]
