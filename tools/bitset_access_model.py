@@ -61,6 +61,54 @@ def mode_of(c, d, list_max=22, bits=352, inline_bits=None):
     return "region"
 
 
+def dir_reads(common, d, c, j, ndir, how):
+    """Directory reads of a region select of the j-th common neighbour at a
+    row with ndir > kPDir 512-bit blocks (the directory dir[g] = commons in
+    blocks < g lives in the region).  Both searches start from the
+    interpolated block g0 = floor(j * ndir / c):
+    * "pair" (the shipped kernel): read dir[g], dir[g+1]; step g by -1 / +1
+      until dir[g] <= j < dir[g+1] (one read per probe);
+    * "sector" (round 3's degree-ordered library): read the 64 B sector of 16
+      entries holding g, move one sector back / forward until the block is
+      inside (one read per sector);
+    * "one": a single read per select (round 3's model)."""
+    if how == "one":
+        return 1
+    blocks = np.bincount(np.asarray(common, dtype=np.int64) // 512, minlength=ndir)[:ndir]
+    dirv = np.concatenate([[0], np.cumsum(blocks)[:-1]])  # commons before block g
+    g = min(int(j * ndir // max(c, 1)), ndir - 1)
+    if how == "pair":
+        reads = 1
+        while True:
+            lo = dirv[g]
+            hi = dirv[g + 1] if g + 1 < ndir else c
+            if j < lo:
+                g -= 1
+            elif j >= hi:
+                g += 1
+            else:
+                return reads
+            reads += 1
+    # "sector"
+    K = 16
+    g &= ~(K - 1)
+    reads, dmv = 0, 0
+    while True:
+        reads += 1
+        E = dirv[g:g + K]
+        cnt = int((E <= j).sum())
+        if cnt == 0:
+            if dmv == 1:
+                return reads
+            g -= K
+            dmv = 2
+        elif cnt == K and g + K < ndir and dmv != 2:
+            g += K
+            dmv = 1
+        else:
+            return reads
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=int, default=20)
@@ -91,6 +139,9 @@ def main():
                          "--tail-filter-bucket filter over positions >= P; selects of the j-th common below the "
                          "prefix count and membership of k < P are answered in registers")
     ap.add_argument("--tail-filter", type=int, default=64)
+    ap.add_argument("--dir-search", default="pair", choices=["pair", "sector", "one"],
+                    help="directory reads of a hub select: the shipped kernel's pair probes, round 3's "
+                         "degree-ordered library's 64 B sectors, or one read (round 3's model)")
     ap.add_argument("--hybrid-dir", type=int, default=1,
                     help="1: entries with 512 < d <= 4096 keep the 128-bit in-entry directory (prefix shrinks by 128)")
     a = ap.parse_args()
@@ -173,8 +224,10 @@ def main():
                             add("sectors_region_select_block")
                             iters[i] += 1
                             if ndir > a.pdir:
-                                add("sectors_region_directory")
-                                iters[i] += 1
+                                nrd = dir_reads(common, d, c, jsel, ndir, a.dir_search)
+                                add("sectors_region_directory", nrd)
+                                add("region_directory_selects")
+                                iters[i] += nrd
                         break
                     add("branch_other")
                 k = index64(u[1], u[2], d)  # the kernel's 64-bit "other" draw (u.y:u.z)
