@@ -201,6 +201,223 @@ struct TsPipeMeta {
   int valid;
 };
 
+struct TsLevelStats {
+  long long ext, upd, maxf;
+};
+
+// ---- PIPE: wave 0 builds the levels of sources[r] into buffer b ---------
+// Same queue order, records and pair updates as the workgroup version in
+// the source loop below; control flow is wave-uniform, lanes exchange
+// through shuffles (child -> parent by a binary search over the chunk's
+// inclusive child counts held one per lane).  The chain of dependent
+// memory round trips is kept short, since the walkers of the previous
+// source saturate the memory system meanwhile: the
+// level-2 pair updates (i = 1: target = child, mid = its parent, both at
+// hand) are computed while the level is filled; deeper even levels rebuild
+// their paths from the level arrays after a fence.
+template <int STEP>
+__device__ __forceinline__ TsLevelStats ts_wave_levels(const TsArgs& A, int b, int64_t r, TsPipeMeta* s_pm) {
+  constexpr int L = 2 * STEP;
+  TsLevelStats st{0, 0, 0};
+  long long& my_ext = st.ext;
+  long long& my_upd = st.upd;
+  long long& my_maxf = st.maxf;
+  const int tid = threadIdx.x;
+  const int64_t blk = blockIdx.x;
+  const gw_dev_graph& G = A.G;
+  const int64_t cap = A.level_cap;
+  const int64_t lvl_stride = (int64_t)(L + 1) * cap;
+  int32_t* V = A.lvl_vertex + blk * 2 * lvl_stride;
+  int32_t* P = A.lvl_parent + blk * 2 * lvl_stride;
+  int32_t* D = A.lvl_deg + blk * 2 * lvl_stride;
+  int64_t* O = A.lvl_off + blk * 2 * lvl_stride;
+  double* M = A.lvl_mass + blk * 2 * cap;
+  int32_t* SN = A.spawn_node + blk * 2 * A.spawn_cap;
+  int32_t* SL = A.spawn_level + blk * 2 * A.spawn_cap;
+  int32_t* SF = A.spawn_first + blk * 2 * (A.spawn_cap + 1);
+  double* SM = A.spawn_mass + blk * 2 * A.spawn_cap;
+  {
+    const int lane = tid & 63;
+    int32_t* Vb = V + b * lvl_stride;
+    int32_t* Pb = P + b * lvl_stride;
+    int32_t* Db = D + b * lvl_stride;
+    int64_t* Ob = O + b * lvl_stride;
+    int32_t* SNb = SN + b * A.spawn_cap;
+    int32_t* SLb = SL + b * A.spawn_cap;
+    int32_t* SFb = SF + b * (A.spawn_cap + 1);
+    double* SMb = SM + b * A.spawn_cap;
+    int32_t* ETb = A.enum_tgt + (blk * 2 + b) * A.enum_cap;
+    double* EVb = A.enum_val + (blk * 2 + b) * A.enum_cap;
+    const int32_t s = A.sources[r];
+    const int ds = G.deg[s];
+    const int64_t os = G.offsets[s];
+    if (lane == 0) {
+      Vb[0] = s;
+      Db[0] = ds;
+      Ob[0] = os;
+      Pb[0] = -1;
+      M[0] = (double)A.sample;  // path[0].sample = SAMPLE (:73)
+    }
+    __threadfence_block();
+    int sz = 1, nsp = 0, nwk = 0, nct = 0;
+    bool abort = false;
+    // record a pair update (target, val) of lanes with tgt >= 0, queue order irrelevant (a sum)
+    auto emit = [&](int32_t tgt, double val) {
+      const unsigned long long em = __ballot(tgt >= 0);
+      const int k = nct + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+      if (tgt >= 0 && k < A.enum_cap) {
+        ETb[k] = tgt;
+        EVb[k] = val;
+      }
+      nct += __popcll(em);
+    };
+    for (int l = 0; l <= L && sz > 0; ++l) {
+      if (lane == 0 && sz > my_maxf) my_maxf = sz;
+      const double* Ml = M + (int64_t)(l & 1) * cap;
+      if ((l & 1) == 0 && l >= 4) {  // computePathSim at pathLen = 2i (:80-83, :157), i >= 2: recorded
+        for (int j0 = 0; j0 < sz; j0 += 64) {
+          const int j = j0 + lane;
+          int32_t tgt = -1;
+          double val = 0.0;
+          if (j < sz) {
+            int32_t path[L + 1], dpath[L + 1];
+            int p = j;
+#pragma unroll
+            for (int t = L; t >= 1; --t) {
+              if (t <= l) {
+                path[t] = Vb[(int64_t)t * cap + p];
+                dpath[t] = Db[(int64_t)t * cap + p];
+                p = Pb[(int64_t)t * cap + p];
+              }
+            }
+            path[0] = s;
+            dpath[0] = ds;
+#pragma unroll
+            for (int t = 4; t <= L; t += 2) {
+              if (t == l) {
+                const int i = t / 2;
+                bool meet = path[t] != s;  // :183
+#pragma unroll
+                for (int q = 0; q < STEP; ++q)  // isFirstMeet (:211-218)
+                  if (q < i && path[q] == path[t - q]) meet = false;
+                if (meet) {
+                  tgt = path[t];
+                  val = ((Ml[j] * A.cache[i]) * (double)dpath[i]) / (double)dpath[t];  // :189
+                  ++my_upd;
+                }
+              }
+            }
+          }
+          emit(tgt, val);
+        }
+        if (nct > A.enum_cap) abort = true;
+      }
+      if (l == L || abort) break;
+      int32_t* Vn = Vb + (int64_t)(l + 1) * cap;
+      int32_t* Pn = Pb + (int64_t)(l + 1) * cap;
+      int32_t* Dn = Db + (int64_t)(l + 1) * cap;
+      int64_t* On = Ob + (int64_t)(l + 1) * cap;
+      double* Mn = M + (int64_t)((l + 1) & 1) * cap;
+      const int32_t* Dl = Db + (int64_t)l * cap;
+      const int64_t* Ol = Ob + (int64_t)l * cap;
+      const bool level2 = l + 1 == 2;  // the children are level 2: record their pair updates now
+      int tot = 0;
+      for (int j0 = 0; j0 < sz; j0 += 64) {
+        const int j = j0 + lane;
+        int cnt = 0, c = 0, d = 0;
+        double m = 0.0;
+        int64_t o = 0;
+        if (j < sz) {
+          d = Dl[j];
+          m = Ml[j];
+          o = Ol[j];
+        }
+        if (d != 0 && m >= (double)d) {  // enumerate (:99)
+          cnt = d;
+        } else if (d != 0) {  // d == 0: randNeighbor() == -1 -> no child (:143-144)
+          c = (int)m;         // number = (int)s == s ? (int)s : (int)s + 1 (:131-135)
+          if ((double)c != m) c += 1;
+        }
+        int ic = cnt, iw = c;  // inclusive wave scans: children, walkers
+#pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+          const int a = __shfl_up(ic, dd, 64), w = __shfl_up(iw, dd, 64);
+          if (lane >= dd) {
+            ic += a;
+            iw += w;
+          }
+        }
+        const int ctot = __shfl(ic, 63, 64), wtot = __shfl(iw, 63, 64);
+        const unsigned long long spm = __ballot(c > 0);
+        const int ksp = nsp + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(spm >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)spm, 0u));
+        if (c > 0 && ksp < A.spawn_cap) {
+          SLb[ksp] = l;
+          SNb[ksp] = j;
+          SFb[ksp] = nwk + iw - c;        // first walker of this spawner (queue order)
+          SMb[ksp] = m / (double)c;      // (double)cur.sample/(double)number (:142)
+        }
+        nsp += __popcll(spm);
+        nwk += wtot;
+        if (nsp > A.spawn_cap || (int64_t)tot + ctot > cap) {
+          abort = true;
+          break;
+        }
+        // the chunk's children, BFS queue order (edges.get(k), insertion order :103-110)
+        for (int c0 = 0; c0 < ctot; c0 += 64) {
+          const int cc = c0 + lane;
+          int pl = 0;  // parent lane: the first lane whose inclusive count exceeds cc
+#pragma unroll
+          for (int st = 32; st >= 1; st >>= 1)
+            if (__shfl(ic, pl + st - 1, 64) <= cc) pl += st;
+          const int pd = __shfl(cnt, pl, 64);
+          const int pex = __shfl(ic, pl, 64) - pd;
+          const int64_t po = ((int64_t)__shfl((int)(o >> 32), pl, 64) << 32) | (uint32_t)__shfl((int)o, pl, 64);
+          const double pm = __shfl(m, pl, 64);
+          int32_t tgt = -1;
+          double val = 0.0;
+          if (cc < ctot) {
+            const gw_ts_ent e = gw_ts_load(A.ent + po + (cc - pex));
+            const int ci = tot + cc;
+            const double cm = pm / (double)pd;  // newSample = cur.sample / degree (:104)
+            Vn[ci] = e.x;
+            Dn[ci] = e.d;
+            On[ci] = e.off;
+            Pn[ci] = j0 + pl;
+            Mn[ci] = cm;
+            if (level2 && e.x != s) {  // i = 1: ((mass * C) * deg(mid)) / deg(target) (:183-189)
+              tgt = e.x;
+              val = ((cm * A.cache[1]) * (double)pd) / (double)e.d;
+              ++my_upd;
+            }
+          }
+          if (level2) emit(tgt, val);
+        }
+        tot += ctot;
+      }
+      if (level2 && nct > A.enum_cap) abort = true;
+      if (abort) break;
+      if (lane == 0) my_ext += tot;
+      sz = tot;
+      __threadfence_block();  // the next level is read back from the level arrays
+    }
+    if (abort && lane == 0) atomicOr(A.error_flag, 1);
+    if (lane == 0) {
+      SFb[abort ? 0 : nsp] = abort ? 0 : nwk;
+      s_pm[b].r = r;
+      s_pm[b].s = s;
+      s_pm[b].ds = ds;
+      s_pm[b].nspawn = abort ? 0 : nsp;
+      s_pm[b].nwalk = abort ? 0 : nwk;
+      s_pm[b].ncontrib = abort ? 0 : min(nct, (int)A.enum_cap);
+      s_pm[b].valid = 1;
+    }
+  }
+  return st;
+}
+
+
 // PIPE (TopSim_singleSample, hash accumulator): the deterministic levels of
 // source s+1 are built by wave 0 alone (wave scans and lane shuffles, no
 // workgroup barrier) into the second half of double-buffered level /
@@ -357,183 +574,19 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     ++my_upd;
   };
 
-  // ---- PIPE: wave 0 builds the levels of sources[r] into buffer b ---------
-  // Same queue order, records and pair updates as the workgroup version in
-  // the source loop below; control flow is wave-uniform, lanes exchange
-  // through shuffles (child -> parent by a binary search over the chunk's
-  // inclusive child counts held one per lane), and the wave's own global
-  // writes are fenced before it reads them back.
-  auto wave_levels = [&](int b, int64_t r) {
-    const int lane = tid & 63;
-    int32_t* Vb = V + b * lvl_stride;
-    int32_t* Pb = P + b * lvl_stride;
-    int32_t* Db = D + b * lvl_stride;
-    int64_t* Ob = O + b * lvl_stride;
-    int32_t* SNb = SN + b * A.spawn_cap;
-    int32_t* SLb = SL + b * A.spawn_cap;
-    int32_t* SFb = SF + b * (A.spawn_cap + 1);
-    double* SMb = SM + b * A.spawn_cap;
-    int32_t* ETb = A.enum_tgt + (blk * 2 + b) * A.enum_cap;
-    double* EVb = A.enum_val + (blk * 2 + b) * A.enum_cap;
-    const int32_t s = A.sources[r];
-    const int ds = G.deg[s];
-    if (lane == 0) {
-      Vb[0] = s;
-      Db[0] = ds;
-      Ob[0] = G.offsets[s];
-      Pb[0] = -1;
-      M[0] = A.sampled;  // path[0].sample = SAMPLE (:73)
-    }
-    __threadfence_block();
-    int sz = 1, nsp = 0, nwk = 0, nct = 0;
-    bool abort = false;
-    for (int l = 0; l <= L && sz > 0; ++l) {
-      if (lane == 0 && sz > my_maxf) my_maxf = sz;
-      const double* Ml = M + (int64_t)(l & 1) * cap;
-      if ((l & 1) == 0 && l >= 2) {  // computePathSim at pathLen = 2i (:80-83, :157): recorded
-        for (int j0 = 0; j0 < sz; j0 += 64) {
-          const int j = j0 + lane;
-          int32_t tgt = -1;
-          double val = 0.0;
-          if (j < sz) {
-            int32_t path[L + 1], dpath[L + 1];
-            int p = j;
-#pragma unroll
-            for (int t = L; t >= 1; --t) {
-              if (t <= l) {
-                path[t] = Vb[(int64_t)t * cap + p];
-                dpath[t] = Db[(int64_t)t * cap + p];
-                p = Pb[(int64_t)t * cap + p];
-              }
-            }
-            path[0] = s;
-            dpath[0] = ds;
-#pragma unroll
-            for (int t = 2; t <= L; t += 2) {
-              if (t == l) {
-                const int i = t / 2;
-                bool meet = path[t] != s;  // :183
-#pragma unroll
-                for (int q = 0; q < STEP; ++q)  // isFirstMeet (:211-218)
-                  if (q < i && path[q] == path[t - q]) meet = false;
-                if (meet) {
-                  tgt = path[t];
-                  val = ((Ml[j] * A.cache[i]) * (double)dpath[i]) / (double)dpath[t];  // :189
-                  ++my_upd;
-                }
-              }
-            }
-          }
-          const unsigned long long em = __ballot(tgt >= 0);
-          const int k = nct + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
-          if (tgt >= 0 && k < A.enum_cap) {
-            ETb[k] = tgt;
-            EVb[k] = val;
-          }
-          nct += __popcll(em);
-        }
-        if (nct > A.enum_cap) abort = true;
-      }
-      if (l == L || abort) break;
-      int32_t* Vn = Vb + (int64_t)(l + 1) * cap;
-      int32_t* Pn = Pb + (int64_t)(l + 1) * cap;
-      int32_t* Dn = Db + (int64_t)(l + 1) * cap;
-      int64_t* On = Ob + (int64_t)(l + 1) * cap;
-      double* Mn = M + (int64_t)((l + 1) & 1) * cap;
-      const int32_t* Dl = Db + (int64_t)l * cap;
-      const int64_t* Ol = Ob + (int64_t)l * cap;
-      int tot = 0;
-      for (int j0 = 0; j0 < sz; j0 += 64) {
-        const int j = j0 + lane;
-        int cnt = 0, c = 0, d = 0;
-        double m = 0.0;
-        int64_t o = 0;
-        if (j < sz) {
-          d = Dl[j];
-          m = Ml[j];
-          o = Ol[j];
-          if (d != 0 && m >= (double)d) {  // enumerate (:99)
-            cnt = d;
-          } else if (d != 0) {  // d == 0: randNeighbor() == -1 -> no child (:143-144)
-            c = (int)m;         // number = (int)s == s ? (int)s : (int)s + 1 (:131-135)
-            if ((double)c != m) c += 1;
-          }
-        }
-        int ic = cnt, iw = c;  // inclusive wave scans: children, walkers
-#pragma unroll
-        for (int dd = 1; dd < 64; dd <<= 1) {
-          const int a = __shfl_up(ic, dd, 64), w = __shfl_up(iw, dd, 64);
-          if (lane >= dd) {
-            ic += a;
-            iw += w;
-          }
-        }
-        const int ctot = __shfl(ic, 63, 64), wtot = __shfl(iw, 63, 64);
-        const unsigned long long spm = __ballot(c > 0);
-        const int ksp = nsp + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(spm >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)spm, 0u));
-        if (c > 0 && ksp < A.spawn_cap) {
-          SLb[ksp] = l;
-          SNb[ksp] = j;
-          SFb[ksp] = nwk + iw - c;        // first walker of this spawner (queue order)
-          SMb[ksp] = m / (double)c;      // (double)cur.sample/(double)number (:142)
-        }
-        nsp += __popcll(spm);
-        nwk += wtot;
-        if (nsp > A.spawn_cap || (int64_t)tot + ctot > cap) {
-          abort = true;
-          break;
-        }
-        // the chunk's children, BFS queue order (edges.get(k), insertion order :103-110)
-        for (int c0 = 0; c0 < ctot; c0 += 64) {
-          const int cc = c0 + lane;
-          int pl = 0;  // parent lane: the first lane whose inclusive count exceeds cc
-#pragma unroll
-          for (int st = 32; st >= 1; st >>= 1)
-            if (__shfl(ic, pl + st - 1, 64) <= cc) pl += st;
-          const int pd = __shfl(cnt, pl, 64);
-          const int pex = __shfl(ic, pl, 64) - pd;
-          const int64_t po = ((int64_t)__shfl((int)(o >> 32), pl, 64) << 32) | (uint32_t)__shfl((int)o, pl, 64);
-          const double pm = __shfl(m, pl, 64);
-          if (cc < ctot) {
-            const gw_ts_ent e = gw_ts_load(A.ent + po + (cc - pex));
-            const int ci = tot + cc;
-            Vn[ci] = e.x;
-            Dn[ci] = e.d;
-            On[ci] = e.off;
-            Pn[ci] = j0 + pl;
-            Mn[ci] = pm / (double)pd;  // newSample = cur.sample / degree (:104)
-          }
-        }
-        tot += ctot;
-      }
-      if (abort) break;
-      if (lane == 0) my_ext += tot;
-      sz = tot;
-      __threadfence_block();
-    }
-    if (abort && lane == 0) atomicOr(A.error_flag, 1);
-    if (lane == 0) {
-      SFb[abort ? 0 : nsp] = abort ? 0 : nwk;
-      s_pm[b].r = r;
-      s_pm[b].s = s;
-      s_pm[b].ds = ds;
-      s_pm[b].nspawn = abort ? 0 : nsp;
-      s_pm[b].nwalk = abort ? 0 : nwk;
-      s_pm[b].ncontrib = abort ? 0 : min(nct, (int)A.enum_cap);
-      s_pm[b].valid = 1;
-    }
-  };
   // PIPE: wave 0 claims the next source and builds its levels into buffer b
   auto claim_and_build = [&](int b) {
     long long r = 0;
     if (tid == 0) r = (long long)atomicAdd(A.src_counter, 1u);
     r = ((long long)__shfl((int)(r >> 32), 0, 64) << 32) | (uint32_t)__shfl((int)r, 0, 64);
-    if (r < A.nsrc)
-      wave_levels(b, (int64_t)r);
-    else if (tid == 0)
+    if (r < A.nsrc) {
+      const TsLevelStats ls = ts_wave_levels<STEP>(A, b, (int64_t)r, s_pm);
+      my_ext += ls.ext;
+      my_upd += ls.upd;
+      if (ls.maxf > my_maxf) my_maxf = ls.maxf;
+    } else if (tid == 0) {
       s_pm[b].valid = 0;
+    }
   };
 
   __shared__ unsigned long long s_ph[11];  // diagnostics only: [10] = last timestamp
@@ -802,6 +855,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     if (PIPE) {
       // wave 0 first builds the next source's levels into the other buffer
       if (tid < 64) claim_and_build(cur ^ 1);
+      mark(0);  // diagnostics: wave 0's level build (the rest of its walker phase goes to "walkers")
       // walkers g < p_nw, then the enumerated nodes' recorded pair updates,
       // dealt out 64 at a time
       const int lane = tid & 63;
