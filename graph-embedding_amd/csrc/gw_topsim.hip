@@ -43,7 +43,6 @@ constexpr int TOPK_MAX = 256;
 constexpr int TS_CO_LDS = 1792;  // child / spawner offsets kept in LDS up to this many entries
 constexpr int64_t LDS_ROW_MAX_BYTES = 96 * 1024;
 constexpr int kPipeMaxSample = 2048;  // k_topsim_pipe for SAMPLE up to this
-constexpr int kRelShift = 47;         // top-k relative pass: bins of 2^47 key units = 1/32 octave
 
 struct TsArgs {
   gw_dev_graph G;
@@ -257,7 +256,11 @@ __device__ __forceinline__ TsLevelStats ts_wave_levels(const TsArgs& A, int b, i
       Db[0] = ds;
       Ob[0] = os;
       Pb[0] = -1;
-      M[0] = (double)A.sample;  // path[0].sample = SAMPLE (:73)
+      // path[0].sample = SAMPLE (:73); converted here, not hoisted out of the
+      // source loop (a loop-invariant double held across the kernel spills)
+      int smp = A.sample;
+      asm volatile("" : "+v"(smp));
+      M[0] = (double)smp;
     }
     __threadfence_block();
     int sz = 1, nsp = 0, nwk = 0, nct = 0;
@@ -444,7 +447,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   __shared__ int s_size[L + 2];
   __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount, s_bin, s_cum, s_exact, s_total,
       s_ncomp, s_all;
-  __shared__ unsigned long long s_prefix, s_mask, s_spbase, s_maxkey;
+  __shared__ unsigned long long s_prefix, s_mask, s_spbase;
   // the output phase's selection arrays share LDS with the levels' child
   // offsets / the walkers' spawner offsets (binary-searched per child / walker)
   __shared__ union {
@@ -490,8 +493,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   double* ov_val = LDS_ROW ? nullptr : (A.ov_vals + blk * A.touch_cap);
   int32_t* touched = LDS_ROW ? nullptr : (A.touched + blk * A.touch_cap);
   const uint32_t ov_mask = (uint32_t)(A.touch_cap - 1);
-  const bool rw = (A.variant == GW_TOPSIM_SINGLE_RW);
-  const bool enumerate_all = (A.variant == GW_TOPSIM_ENUMERATE);
+  const bool rw = !PIPE && (A.variant == GW_TOPSIM_SINGLE_RW);  // PIPE: TopSim_singleSample only
+  const bool enumerate_all = !PIPE && (A.variant == GW_TOPSIM_ENUMERATE);
 
   long long my_ext = 0, my_upd = 0, my_walk = 0, my_maxf = 0;
 
@@ -688,7 +691,6 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       if (tid == 0) {
         s_wnext = 0u;
         s_ncomp = 0;
-        s_maxkey = 0ull;
       }
       __syncthreads();
     } else {
@@ -696,7 +698,6 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       s_src = (int)atomicAdd(A.src_counter, 1u);
       s_abort = 0;
       s_ncomp = 0;
-      s_maxkey = 0ull;
     }
     __syncthreads();
     r = s_src;
@@ -915,21 +916,12 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       int32_t kk[SPT];
       double vv[SPT];
       int mine = 0;
-      unsigned long long mk = 0ull;  // the row's largest key (the top-k's relative pass below)
 #pragma unroll
       for (int i = 0; i < SPT; ++i) {
         kk[i] = s_hkey[tid + i * BLOCK];
         vv[i] = s_hval[tid + i * BLOCK];
         mine += kk[i] != -1;
-        if (kk[i] != -1 && dkey(vv[i]) > mk) mk = dkey(vv[i]);
       }
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) {
-        const unsigned long long y = ((unsigned long long)(uint32_t)__shfl_xor((int)(mk >> 32), d, 64) << 32) |
-                                     (uint32_t)__shfl_xor((int)mk, d, 64);
-        if (y > mk) mk = y;
-      }
-      if ((tid & 63) == 0 && mk) atomicMax(&s_maxkey, mk);
       // offsets: an inclusive scan inside the wave and one LDS atomic per
       // wave (the compacted order is free: selection and the sparse-row
       // writer do not depend on it); the barrier orders every read before the writes
@@ -1035,45 +1027,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       bool take_all = false;     // at most K candidates (counted by the first radix pass)
       bool bin_exact = false;    // the K-th key's bin is taken whole: select by masked prefix
       unsigned long long Tmask = ~0ull;
-      // hash mode: ONE histogram pass over the key's distance below the row
-      // maximum (found during compaction), 32 bins per octave over 8 octaves.
-      // The top byte of a positive double is its sign and high exponent bits,
-      // so the raw radix's first pass barely splits a row of scores within a
-      // few octaves; the relative pass leaves the K-th key's bin with a few
-      // entries, taken whole and ranked below.  Falls back to the raw radix
-      // when that bin is the clamped one or too full (or overflow entries live
-      // in HBM).
-      bool rel_exact = false;
-      unsigned long long Trel = 0;  // selected: key > Trel
-      if (!LDS_ROW && nov == 0) {
-        if (NC <= K) {
-          take_all = true;
-        } else {
-          const unsigned long long mx = s_maxkey;
-          for (int b = tid; b < 256; b += BLOCK) s_hist[b] = 0;
-          if (tid == 0) s_exact = 0;
-          __syncthreads();
-          for (int idx = tid; idx < NC; idx += BLOCK) {
-            int32_t id;
-            double v;
-            if (!cand(idx, &id, &v)) continue;
-            const unsigned long long dk = (mx - dkey(v)) >> kRelShift;
-            atomicAdd(&s_hist[dk < 255ull ? (int)dk : 255], 1u);
-          }
-          __syncthreads();
-          if (tid < 64) {
-            select_bin(s_hist, K, false, &s_bin, &s_cum);
-            if (tid == 0 && s_bin < 255 && s_cum + (int)s_hist[s_bin] <= kcoll) s_exact = 1;
-          }
-          __syncthreads();
-          if (s_exact) {
-            rel_exact = true;
-            const unsigned long long span = (unsigned long long)(s_bin + 1) << kRelShift;
-            Trel = mx >= span ? mx - span : 0ull;
-          }
-        }
-      }
-      if (!take_all && !rel_exact) {
+      {
         for (int b = tid; b < 256; b += BLOCK) s_hist[b] = 0;
         if (tid == 0) {
           s_prefix = 0;
@@ -1127,7 +1081,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         T = s_prefix;
       }
       mark(6);
-      if (!take_all && !rel_exact && !bin_exact) {
+      if (!take_all && !bin_exact) {
         // ties at the threshold: smallest ids first
         long long eq_local = 0;
         for (int idx = tid; idx < NC; idx += BLOCK) {
@@ -1169,14 +1123,25 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       mark(7);
       if (tid == 0) s_cnt = 0;
       __syncthreads();
-      for (int idx = tid; idx < NC; idx += BLOCK) {
-        int32_t id;
-        double v;
-        if (!cand(idx, &id, &v)) continue;
-        const unsigned long long k = dkey(v);
-        if (take_all || (rel_exact ? k > Trel : bin_exact ? (k & Tmask) >= T : (k > T || (k == T && id <= idT)))) {
-          int slot = atomicAdd(&s_cnt, 1);
-          if (slot < TOPK_MAX) {
+      // one LDS atomic per wave and round (ballot + v_mbcnt ranks), not one
+      // per selected entry on the same counter
+      for (int base = 0; base < NC; base += BLOCK) {
+        const int idx = base + tid;
+        int32_t id = 0;
+        double v = 0.0;
+        bool sel = false;
+        if (idx < NC && cand(idx, &id, &v)) {
+          const unsigned long long k = dkey(v);
+          sel = take_all || (bin_exact ? (k & Tmask) >= T : (k > T || (k == T && id <= idT)));
+        }
+        const unsigned long long sm = __ballot(sel);
+        if (sm) {
+          int wb = 0;
+          if ((tid & 63) == __ffsll(sm) - 1) wb = atomicAdd(&s_cnt, __popcll(sm));
+          wb = __shfl(wb, __ffsll(sm) - 1, 64);
+          const int slot = wb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+          if (sel && slot < TOPK_MAX) {
             s_sel_id[slot] = id;
             s_sel_val[slot] = v;
           }
