@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--rebuild", type=int, default=2)
     ap.add_argument("--mode", default="bitset")
+    ap.add_argument("--listed", type=int, default=-1,
+                    help="gw_options_t.listed for the rejection sampler (0: plain 16 B entries, k_walk_scale)")
     a = ap.parse_args()
     import torch
     from gwamd import _lib as C
@@ -76,6 +78,11 @@ def main():
             C.check(L.gw_graph_rmat(a.scale, a.ef, 0.57, 0.19, 0.19, 42, ctypes.byref(h)))
             if L.gw_graph_to_device(h, 0) != 0:
                 raise SystemExit(L.gw_last_error(h).decode())
+            if a.listed != -1:
+                o = C.Options()
+                C.check(L.gw_graph_get_options(h, ctypes.byref(o)))
+                o.listed = a.listed
+                C.check(L.gw_graph_set_options(h, ctypes.byref(o)))
             t0 = time.perf_counter()
             if L.gw_n2v_prepare(h, a.p, a.q, mode) != 0:
                 raise SystemExit(L.gw_last_error(h).decode())
