@@ -206,8 +206,7 @@ struct N2VParams {
   double h_prev;     // min(1/p, M): in-envelope height of the return edge
   uint32_t k0, k1;   // step key
   uint32_t pk0, pk1; // permutation key
-  uint32_t diag;     // timing experiments only: 1 no walk output stores (GW_DIAG_NO_STORE=1),
-                     // 2 has_edge probes at once, not deferred (GW_DIAG_NO_DEFER=1)
+  uint32_t diag;     // timing experiments only (GW_DIAG_NO_STORE=1: no walk output stores)
   // mixture proposal (unweighted undirected, q > 1; see k_walk_scale)
   double mix_o;       // outlier mass of the return edge: max(0, 1/p - 1/q)
   double mix_p;       // mass per vertex of the prev branch: 1 - 1/q
@@ -344,16 +343,6 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
   int64_t nb = 0;  // candidate's row (slot entries)
   int32_t nd = 0;
   double Wcur = 0.0;
-  // Deferred has_edge probe (undirected): the candidate's entry arrives in one
-  // iteration, its probe is issued in the next one beside the other lanes'
-  // loads, so no iteration of the wave-uniform loop waits for two dependent
-  // round trips.  pend: 0 none, 1 x in N(prev) (uniform proposal), 2 x in
-  // N(cur) (mixture, prev branch); pslot: the candidate's slot.  Same draws
-  // and decisions as probing at once: the walks do not change.
-  uint32_t pend = 0u;
-  int64_t pslot = 0;
-  int32_t next_c = -1;  // the pending candidate
-  const bool defer = !DIRECTED && !(kGwDiag && (P.diag & 2u));
   if (valid) {
     const uint64_t it = (uint64_t)w / (uint64_t)G.n;
     const uint64_t pos = (uint64_t)w % (uint64_t)G.n;
@@ -376,15 +365,7 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
       bool acc;
       int64_t slot;
       int32_t next;
-      if (!FIRST_ORDER && !DIRECTED && pend) {  // the deferred probe of last iteration's candidate
-        const bool adj = pend == 1u ? gw_has_edge(G, pb, pe, next_c) : gw_has_edge(G, b, e, next_c);
-        // uniform proposal, t >= min(1, 1/q): accepted iff x is common (q > 1) / not common (q < 1)
-        acc = pend == 1u ? ((P.a_q < 1.0) ? adj : !adj) : adj;
-        if (pend == 1u && trial >= (1u << 24)) acc = true;
-        slot = pslot;
-        next = next_c;
-        pend = 0u;
-      } else if (FIRST_ORDER || len == 1) {
+      if (FIRST_ORDER || len == 1) {
         gw_u4 u = gw_philox(c0, c1, (uint32_t)len, 0u, P.k0, P.k1);
         trial = 1;
         slot = b + draw_first_order<WEIGHTED>(G, b, d, u.x, u.z, u.y);
@@ -419,18 +400,10 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
           } else {
             next = G.nbrs[slot];
           }
-          if (from_cur) {
+          if (from_cur)
             acc = next != prev || gw_u01(u.w) < P.mix_prev;
-          } else if (next == prev) {
-            acc = false;
-          } else if (defer) {  // x in N(cur): probed next iteration
-            acc = false;
-            pend = 2u;
-            pslot = slot;
-            next_c = next;
-          } else {
-            acc = gw_has_edge(G, b, e, next);  // x in N(cur)
-          }
+          else
+            acc = next != prev && gw_has_edge(G, b, e, next);  // x in N(cur)
           if (trial >= (1u << 24) && from_cur) acc = true;
         }
       } else {
@@ -461,11 +434,6 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
             acc = t < P.h_prev;
           } else if (t < P.lo) {
             acc = true;
-          } else if (defer) {  // x in N(prev): probed next iteration
-            acc = false;
-            pend = 1u;
-            pslot = slot;
-            next_c = next;
           } else {
             bool adj;
             if (DIRECTED)
@@ -475,7 +443,7 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
               adj = gw_has_edge(G, pb, pe, next);  // x in N(prev)
             acc = t < (adj ? 1.0 : P.a_q);
           }
-          if (trial >= (1u << 24) && !pend) acc = true;
+          if (trial >= (1u << 24)) acc = true;
         }
       }
       if (acc) {
@@ -527,7 +495,7 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
     // cost up to 22% of a launch: GW_DIAG_NO_STORE A/B), and the ready
     // walkers are compacted first: ceil(ready / 16) rounds, not 4
     const unsigned long long rm = __ballot(ready);
-    if (rm && !(kGwDiag && (P.diag & 1u))) {
+    if (rm && !(kGwDiag && P.diag)) {
       if (vec_ok) {
         const int nready = __popcll(rm);
         int32_t* ids = s_ids[threadIdx.x >> 6];
@@ -1062,8 +1030,7 @@ int gw_dev_n2v_walks(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int6
   P.pk1 = (uint32_t)(seed >> 32) ^ GW_TAG_N2V_PERM;
   {
     const char* ns = GW_DIAG_ENV("GW_DIAG_NO_STORE");
-    const char* nd = GW_DIAG_ENV("GW_DIAG_NO_DEFER");
-    P.diag = ((ns && ns[0] == '1') ? 1u : 0u) | ((nd && nd[0] == '1') ? 2u : 0u);
+    P.diag = (ns && ns[0] == '1') ? 1u : 0u;
   }
   if (g->n2v_mode == GW_N2V_BITSET && !first_order)
     return gw_dev_walk_bitset_launch(g, L, seed, walk_begin, walk_count, shuffle, out_dev, len_dev, counters_dev,
