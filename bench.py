@@ -697,7 +697,9 @@ def walk_kernel_name(mode, G):
     inf = G.info()
     if mode == "rejection" and inf.sampler_bytes >= 64 * inf.nnz:
         return "k_walk_listed"
-    return "k_walk_scale"
+    # the template's first argument tells first-order launches from second-order
+    # ones of the same grid (a secondary also times the rejection sampler on its graph)
+    return "k_walk_scale<true" if mode == "first-order" else "k_walk_scale<false"
 
 
 def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejection=False, walks_per_node=1,
@@ -873,7 +875,7 @@ def topsim_roofline(ext, upd, kt, tag, nsrc, nnz, step):
             "traffic": prof["hbm_bytes_per_launch"] if prof else None,
             "traffic_GBps": prof["hbm_bytes_per_launch"] / kt / 1e9 if prof else None,
             "algorithmic_bytes": alg, "slot_table_bytes": table, "kernel": "k_topsim", "kernel_ms": kt * 1e3,
-            "units_per_launch": nsrc, "pmc_tag": tag, "pmc_match": {"kernel": f"k_topsim(_2wg)?<{step},", "grid": None},
+            "units_per_launch": nsrc, "pmc_tag": tag, "pmc_match": {"kernel": f"k_topsim(_2wg|_pipe|_pipe_row)?<{step}[,>]", "grid": None},
             "random_line_roofline": line_roofline(prof, kt, table, 128)}
 
 

@@ -45,9 +45,9 @@ def main():
             srcs = np.nonzero(deg > 0)[0].astype(np.int32)
             K, sample, step = 100, 1000, 3
         else:
-            V = 38741
-            g = topsim.Graph(os.path.join(ROOT, "tests", "golden", "data", "arxiv_author_pub.txt"), V,
-                             separator="\t", device=0)
+            f, V, sep = {"arxiv": ("arxiv_author_pub.txt", 38741, "\t"), "blog": ("blog.txt", 10313, ","),
+                         "moreno": ("moreno_crime_crime.txt", 1380, "\t")}[name]
+            g = topsim.Graph(os.path.join(ROOT, "tests", "golden", "data", f), V, separator=sep, device=0)
             g._ensure_device()
             h = g._g.handle
             srcs = np.arange(V, dtype=np.int32)
