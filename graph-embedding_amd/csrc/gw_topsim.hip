@@ -1240,12 +1240,6 @@ __global__ void __launch_bounds__(TS_BLOCK) __attribute__((amdgpu_waves_per_eu(4
   topsim_body<STEP, 2, TS_BLOCK, true>(A);
 }
 
-// pipelined, dense LDS row over 72 KB (one workgroup per CU)
-template <int STEP>
-__global__ void __launch_bounds__(TS_BLOCK) k_topsim_pipe_row(TsArgs A) {
-  topsim_body<STEP, 0, TS_BLOCK, true>(A);
-}
-
 template <typename T>
 int ws_alloc(gw_graph* g, T** p, int64_t count) {
   *p = nullptr;
@@ -1297,13 +1291,6 @@ hipError_t launch_mode(int mode, bool pipe, const TsArgs& A, int blocks, size_t 
                                        (int)lds);
     if (e != hipSuccess) return e;
     k_topsim_pipe<STEP><<<blocks, TS_BLOCK, lds, s>>>(A);
-    return hipGetLastError();
-  }
-  if (mode == 0 && pipe) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_topsim_pipe_row<STEP>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    k_topsim_pipe_row<STEP><<<blocks, TS_BLOCK, lds, s>>>(A);
     return hipGetLastError();
   }
   if (mode == 2) return launch_step<STEP, 2, true>(A, blocks, lds, s);
@@ -1406,9 +1393,6 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   bool pipe = variant == GW_TOPSIM_SINGLE_SAMPLE && mode == 2 && sample <= kPipeMaxSample;
   if (const char* np = GW_DIAG_ENV("GW_DIAG_TS_NOPIPE"))  // A/B knob: the unpipelined kernel
     if (np[0] == '1') pipe = false;
-  // A/B knob (diag library): pipelined dense LDS row (one workgroup per CU, any SAMPLE)
-  if (const char* pr = GW_DIAG_ENV("GW_DIAG_TS_PIPE_ROW"))
-    if (pr[0] == '1' && variant == GW_TOPSIM_SINGLE_SAMPLE && mode == 0 && (size_t)n * 8 > TS_2WG_LDS) pipe = true;
   const int64_t nb = pipe ? 2 : 1;
   const int64_t enum_cap = pipe ? (int64_t)step * level_cap : 1;
   const int64_t per_block = nb * ((int64_t)(L + 1) * level_cap * 20 + spawn_cap * 20 + 4) + 2 * level_cap * 8 +
