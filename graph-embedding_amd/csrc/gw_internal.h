@@ -123,6 +123,8 @@ struct gw_topsim_ws {
   int64_t enum_cap = 0;           // enumerated-node pair updates per source (pipelined kernel)
   int32_t* enum_tgt = nullptr;    // [blocks][2][enum_cap]
   double* enum_val = nullptr;     // [blocks][2][enum_cap]
+  int32_t* dsel_id = nullptr;     // [blocks][TOPK_MAX] pipelined kernel: selected entries awaiting order
+  double* dsel_val = nullptr;
   unsigned int* src_counter = nullptr;  // work queue head
   int* error_flag = nullptr;      // capacity overflow
 };

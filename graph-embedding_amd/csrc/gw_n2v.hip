@@ -585,6 +585,8 @@ void gw_dev_release(gw_graph* g) {
   dev_free(t.touched);
   dev_free(t.enum_tgt);
   dev_free(t.enum_val);
+  dev_free(t.dsel_id);
+  dev_free(t.dsel_val);
   dev_free(t.src_counter);
   dev_free(t.error_flag);
   t = gw_topsim_ws();

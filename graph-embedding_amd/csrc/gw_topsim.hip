@@ -48,7 +48,8 @@ struct TsArgs {
   gw_dev_graph G;
   int variant;
   int diag;  // GW_DIAG_TS (timing experiments only, wrong results): 1 = walkers skip computePathSim, 2 = cheap RNG,
-             // 4 / 8 = walker reads confined to the first 2^26 / 2^27 slot entries
+             // 4 / 8 = walker reads confined to the first 2^26 / 2^27 slot entries;
+             // A/B knob (same results): 32 = no deferred ordering
   int sample;
   double sampled;
   double cache[16];
@@ -78,6 +79,8 @@ struct TsArgs {
   int32_t* enum_tgt;  // pipelined kernel: enumerated-node pair updates of a source, [blocks][2][enum_cap]
   double* enum_val;
   int64_t enum_cap;
+  int32_t* dsel_id;  // pipelined kernel, top-k rows: a source's selected entries awaiting order, [blocks][TOPK_MAX]
+  double* dsel_val;
   int32_t* touched;
   unsigned int* src_counter;
   int* error_flag;
@@ -135,13 +138,14 @@ __device__ __forceinline__ int upper_bound_i32(const int32_t* a, int n, int x) {
   return lo;
 }
 
-// wave 0 of the block: the radix bin holding the need-th key, scanning the
-// 256 bins from the top (desc) or from the bottom (asc); 4 bins per lane and
-// one wave scan instead of a serial 256-step loop.  Returns (bin, keys in
-// the bins scanned before it) through *bin / *before (lane 0 writes them).
-__device__ __forceinline__ void select_bin(const unsigned* hist, int need, bool desc, int* bin, int* before,
-                                           int* total = nullptr) {
-  const int lane = threadIdx.x & 63;
+// one wave: the radix bin holding the need-th key, scanning the 256 bins
+// from the top (desc) or from the bottom (asc); 4 bins per lane and one wave
+// scan instead of a serial 256-step loop.  Every lane gets (bin, keys in the
+// bins scanned before it, keys in all bins).
+__device__ __forceinline__ void select_bin_w(const unsigned* hist, int need, bool desc, int& bin, int& before,
+                                             int& total) {
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));  // its bin addresses formed per call, not held across the kernel
   int c[4], loc = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -167,10 +171,18 @@ __device__ __forceinline__ void select_bin(const unsigned* hist, int need, bool 
   const unsigned long long m = __ballot(first >= 0);
   const int src = m ? __ffsll(m) - 1 : 63;
   const int o = __shfl(first >= 0 ? first : 255, src, 64);
-  const int cb = __shfl(first >= 0 ? cum_at : run - c[3], src, 64);
-  const int tot = __shfl(inc, 63, 64);
-  if (lane == 0) {
-    *bin = desc ? 255 - o : o;
+  before = __shfl(first >= 0 ? cum_at : run - c[3], src, 64);
+  total = __shfl(inc, 63, 64);
+  bin = desc ? 255 - o : o;
+}
+
+// the same, lane 0 storing the results (wave 0 for the whole workgroup)
+__device__ __forceinline__ void select_bin(const unsigned* hist, int need, bool desc, int* bin, int* before,
+                                           int* total = nullptr) {
+  int b, cb, tot;
+  select_bin_w(hist, need, desc, b, cb, tot);
+  if ((threadIdx.x & 63) == 0) {
+    *bin = b;
     *before = cb;
     if (total) *total = tot;
   }
@@ -178,6 +190,56 @@ __device__ __forceinline__ void select_bin(const unsigned* hist, int need, bool 
 
 __device__ __forceinline__ unsigned long long dkey(double v) {
   return (unsigned long long)__double_as_longlong(v);  // v >= 0: bit order == value order
+}
+
+// One wave, no workgroup barrier: the cnt (<= TOPK_MAX) selected (id, value)
+// entries sid / sval ranked (value desc, id asc — the FixedMaxPQ /
+// Print.printByOrder order, FixedMaxPQ.java:30-39), ranks < K written to
+// oid / osc, -1 / 0 padded.  The pipelined kernel's deferred ordering: the
+// workgroup selects source s's top entries, and one wave ranks them while
+// the others walk source s + 1.
+__device__ __forceinline__ void ts_wave_rank(const int32_t* sid, const double* sval, int cnt, int K, int32_t* oid,
+                                             double* osc) {
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));  // per-lane addresses formed here, not hoisted out of the source loop
+  constexpr int Q = TOPK_MAX / 64;
+  int32_t mi[Q];
+  double mv[Q];
+  int rk[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int idx = q * 64 + lane;
+    mi[q] = idx < cnt ? sid[idx] : 0x7fffffff;
+    mv[q] = idx < cnt ? sval[idx] : -1.0;
+    rk[q] = 0;
+  }
+  // rank = entries before it in (value desc, id asc); sources broadcast by readlane
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    if (q * 64 < cnt) {
+      const int m = min(64, cnt - q * 64);
+      const long long mvb = __double_as_longlong(mv[q]);
+      for (int src = 0; src < m; ++src) {
+        const int lo = __builtin_amdgcn_readlane((int)mvb, src);
+        const int hi = __builtin_amdgcn_readlane((int)(mvb >> 32), src);
+        const double vj = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+        const int32_t ij = __builtin_amdgcn_readlane(mi[q], src);
+#pragma unroll
+        for (int qq = 0; qq < Q; ++qq)
+          if (qq * 64 < cnt) rk[qq] += (vj > mv[qq]) || (vj == mv[qq] && ij < mi[qq]);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+    if (q * 64 + lane < cnt && rk[q] < K) {
+      oid[rk[q]] = mi[q];
+      osc[rk[q]] = mv[q];
+    }
+  for (int k = min(cnt, K) + lane; k < K; k += 64) {
+    oid[k] = -1;
+    osc[k] = 0.0;
+  }
 }
 
 // MODE 0: dense LDS row; 1: LDS hash of 8192 slots (96 KB, one workgroup per
@@ -237,7 +299,11 @@ __device__ __forceinline__ TsLevelStats ts_wave_levels(const TsArgs& A, int b, i
   int32_t* SF = A.spawn_first + blk * 2 * (A.spawn_cap + 1);
   double* SM = A.spawn_mass + blk * 2 * A.spawn_cap;
   {
-    const int lane = tid & 63;
+    // opaque per source: the per-lane array addresses below are then formed
+    // here, not hoisted out of the kernel's source loop as 64-bit VGPR pairs
+    // held across the walkers (one of them spilled at the 128-VGPR cap)
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
     int32_t* Vb = V + b * lvl_stride;
     int32_t* Pb = P + b * lvl_stride;
     int32_t* Db = D + b * lvl_stride;
@@ -435,6 +501,9 @@ template <int STEP, int MODE, int BLOCK = TS_BLOCK, bool PIPE = false>
 __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   constexpr int NW = BLOCK / 64;
   constexpr int NB = PIPE ? 2 : 1;  // level / spawner scratch buffers per workgroup
+  // pipelined kernel: a source's top-k ordered by one wave during the next
+  // source's walkers (deferred ordering)
+  constexpr bool DEFER = PIPE;
   constexpr int CO_LDS = TS_CO_LDS;
   constexpr bool LDS_ROW = MODE == 0;
   using H = TsHash<MODE>;
@@ -497,6 +566,15 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   const bool enumerate_all = !PIPE && (A.variant == GW_TOPSIM_ENUMERATE);
 
   long long my_ext = 0, my_upd = 0, my_walk = 0, my_maxf = 0;
+  // deferred ordering of the top-k rows (the dense / sparse row writers keep the in-place phase)
+  const bool defer = DEFER && A.out_ids && !(kGwDiag && (A.diag & 32));
+  int64_t pend_r = -1;  // the source whose selected entries await ranking
+  int pend_n = 0;
+  auto deferred_topk = [&]() {
+    const int K = A.topk;
+    ts_wave_rank(A.dsel_id + blk * TOPK_MAX, A.dsel_val + blk * TOPK_MAX, pend_n, K,
+                 A.out_ids + pend_r * (int64_t)K, A.out_scores + pend_r * (int64_t)K);
+  };
 
   if (LDS_ROW) {
     for (int j = tid; j < n; j += BLOCK) s_row[j] = 0.0;
@@ -858,7 +936,10 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     // random walkers: one lane each, path in registers
     if (PIPE) {
       // wave 0 first builds the next source's levels into the other buffer
-      if (tid < 64) claim_and_build(cur ^ 1);
+      if (tid < 64)
+        claim_and_build(cur ^ 1);
+      else if (defer && pend_r >= 0 && tid >= BLOCK - 64)
+        deferred_topk();  // the last wave ranks the previous source meanwhile
       mark(0);  // diagnostics: wave 0's level build (the rest of its walker phase goes to "walkers")
       // walkers g < p_nw, then the enumerated nodes' recorded pair updates,
       // dealt out 64 at a time
@@ -1150,38 +1231,49 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       __syncthreads();
       const int cnt = min(s_cnt, TOPK_MAX);
       mark(8);
-      // order by (value desc, id asc): every selected entry counts the entries
-      // that precede it (<= 256 entries, one pass, broadcast LDS reads)
-      int32_t* oid = A.out_ids + r * (int64_t)K;
-      double* osc = A.out_scores + r * (int64_t)K;
-      {
-        // G threads per entry (4 while cnt <= BLOCK / 4, then 2, then 1; more
-        // entries than threads take several passes), partial counts summed with lane shuffles
-        const int G = cnt <= BLOCK / 4 ? 4 : cnt <= BLOCK / 2 ? 2 : 1;
-        for (int i0 = 0; i0 < cnt; i0 += BLOCK / G) {
-          const int i = i0 + tid / G, sub = tid % G;
-          int rank = 0;
-          double vi = 0.0;
-          int32_t ii = 0;
-          if (i < cnt) {
-            vi = s_sel_val[i];
-            ii = s_sel_id[i];
-#pragma unroll 4
-            for (int j = sub; j < cnt; j += G) {
-              const double vj = s_sel_val[j];
-              rank += (vj > vi) || (vj == vi && s_sel_id[j] < ii);
+      if (defer) {
+        // deferred ordering: the selected entries go to the workgroup's HBM
+        // scratch; the last wave ranks them during the next walker phase
+        for (int k = tid; k < cnt; k += BLOCK) {
+          A.dsel_id[blk * TOPK_MAX + k] = s_sel_id[k];
+          A.dsel_val[blk * TOPK_MAX + k] = s_sel_val[k];
+        }
+        pend_r = r;
+        pend_n = cnt;
+      } else {
+        // order by (value desc, id asc): every selected entry counts the entries
+        // that precede it (<= 256 entries, one pass, broadcast LDS reads)
+        int32_t* oid = A.out_ids + r * (int64_t)K;
+        double* osc = A.out_scores + r * (int64_t)K;
+        {
+          // G threads per entry (4 while cnt <= BLOCK / 4, then 2, then 1; more
+          // entries than threads take several passes), partial counts summed with lane shuffles
+          const int G = cnt <= BLOCK / 4 ? 4 : cnt <= BLOCK / 2 ? 2 : 1;
+          for (int i0 = 0; i0 < cnt; i0 += BLOCK / G) {
+            const int i = i0 + tid / G, sub = tid % G;
+            int rank = 0;
+            double vi = 0.0;
+            int32_t ii = 0;
+            if (i < cnt) {
+              vi = s_sel_val[i];
+              ii = s_sel_id[i];
+  #pragma unroll 4
+              for (int j = sub; j < cnt; j += G) {
+                const double vj = s_sel_val[j];
+                rank += (vj > vi) || (vj == vi && s_sel_id[j] < ii);
+              }
+            }
+            for (int o = 1; o < G; o <<= 1) rank += __shfl_xor(rank, o, 64);
+            if (i < cnt && sub == 0 && rank < K) {
+              oid[rank] = ii;
+              osc[rank] = vi;
             }
           }
-          for (int o = 1; o < G; o <<= 1) rank += __shfl_xor(rank, o, 64);
-          if (i < cnt && sub == 0 && rank < K) {
-            oid[rank] = ii;
-            osc[rank] = vi;
-          }
         }
-      }
-      for (int k = min(cnt, K) + tid; k < K; k += BLOCK) {
-        oid[k] = -1;
-        osc[k] = 0.0;
+        for (int k = min(cnt, K) + tid; k < K; k += BLOCK) {
+          oid[k] = -1;
+          osc[k] = 0.0;
+        }
       }
     }
     __syncthreads();
@@ -1209,6 +1301,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     mark(4);
     if (PIPE) cur ^= 1;
   }
+  if (defer && pend_r >= 0 && tid >= BLOCK - 64) deferred_topk();  // the workgroup's last source
 
   if (kGwDiag && A.phase && tid == 0)
     for (int k = 0; k < 10; ++k) atomicAdd(&A.phase[k], s_ph[k]);
@@ -1238,6 +1331,12 @@ __global__ void __launch_bounds__(TS_BLOCK) __attribute__((amdgpu_waves_per_eu(4
 template <int STEP>
 __global__ void __launch_bounds__(TS_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) k_topsim_pipe(TsArgs A) {
   topsim_body<STEP, 2, TS_BLOCK, true>(A);
+}
+
+// pipelined, dense LDS row over 72 KB (one workgroup per CU)
+template <int STEP>
+__global__ void __launch_bounds__(TS_BLOCK) k_topsim_pipe_row(TsArgs A) {
+  topsim_body<STEP, 0, TS_BLOCK, true>(A);
 }
 
 template <typename T>
@@ -1291,6 +1390,13 @@ hipError_t launch_mode(int mode, bool pipe, const TsArgs& A, int blocks, size_t 
                                        (int)lds);
     if (e != hipSuccess) return e;
     k_topsim_pipe<STEP><<<blocks, TS_BLOCK, lds, s>>>(A);
+    return hipGetLastError();
+  }
+  if (mode == 0 && pipe) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_topsim_pipe_row<STEP>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    k_topsim_pipe_row<STEP><<<blocks, TS_BLOCK, lds, s>>>(A);
     return hipGetLastError();
   }
   if (mode == 2) return launch_step<STEP, 2, true>(A, blocks, lds, s);
@@ -1348,6 +1454,8 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   ws_free(t.touched);
   ws_free(t.enum_tgt);
   ws_free(t.enum_val);
+  ws_free(t.dsel_id);
+  ws_free(t.dsel_val);
   ws_free(t.src_counter);
   ws_free(t.error_flag);
   const int64_t n = g->n;
@@ -1390,13 +1498,19 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   // small next to the walkers — P10M, SAMPLE 1000: ~130 enumerated nodes and
   // ~1,060 walkers per source — not for SAMPLE in the thousands on low-degree
   // graphs, whose levels reach thousands of nodes)
-  bool pipe = variant == GW_TOPSIM_SINGLE_SAMPLE && mode == 2 && sample <= kPipeMaxSample;
+  // The dense LDS row over 72 KB (one workgroup per CU, e.g. blog) runs
+  // pipelined at any SAMPLE: its single workgroup otherwise leaves the CU idle
+  // of walker reads during every level / output phase (blog, SAMPLE 10000:
+  // 10.32 vs 10.52 ms, profiles/r04/ts_knob_ab_defer_order_pipe_row.jsonl).
+  bool pipe = variant == GW_TOPSIM_SINGLE_SAMPLE &&
+              ((mode == 2 && sample <= kPipeMaxSample) || (mode == 0 && (size_t)n * 8 > TS_2WG_LDS));
   if (const char* np = GW_DIAG_ENV("GW_DIAG_TS_NOPIPE"))  // A/B knob: the unpipelined kernel
     if (np[0] == '1') pipe = false;
   const int64_t nb = pipe ? 2 : 1;
   const int64_t enum_cap = pipe ? (int64_t)step * level_cap : 1;
   const int64_t per_block = nb * ((int64_t)(L + 1) * level_cap * 20 + spawn_cap * 20 + 4) + 2 * level_cap * 8 +
-                            (level_cap + 1) * 4 + (pipe ? 2 * enum_cap * 12 : 0) + (lds_row ? 0 : touch_cap * 16);
+                            (level_cap + 1) * 4 + (pipe ? 2 * enum_cap * 12 : 0) +
+                            (lds_row ? 0 : touch_cap * 16) + (pipe ? TOPK_MAX * 12 : 0);
   int dev_cus = 256;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, g->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
@@ -1421,6 +1535,8 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
       (rc = ws_alloc(g, &t.enum_tgt, blocks * 2 * enum_cap)) ||
       (rc = ws_alloc(g, &t.enum_val, blocks * 2 * enum_cap)) ||
       (rc = ws_alloc(g, &t.touched, blocks * touch_cap)) ||
+      (rc = ws_alloc(g, &t.dsel_id, pipe ? blocks * TOPK_MAX : 1)) ||
+      (rc = ws_alloc(g, &t.dsel_val, pipe ? blocks * TOPK_MAX : 1)) ||
       (rc = ws_alloc(g, &t.src_counter, 1)) || (rc = ws_alloc(g, &t.error_flag, 1)))
     return rc;
   if (!t.ent && g->nnz > 0) {  // slot entries {x, deg(x), offsets[x]}: one random line per path extension
@@ -1503,6 +1619,8 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   A.enum_tgt = t.enum_tgt;
   A.enum_val = t.enum_val;
   A.enum_cap = t.enum_cap;
+  A.dsel_id = t.dsel_id;
+  A.dsel_val = t.dsel_val;
   A.touched = t.touched;
   A.src_counter = t.src_counter;
   A.error_flag = t.error_flag;

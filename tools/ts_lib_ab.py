@@ -7,6 +7,12 @@ every variant with the first (fp64 atomics make the last bits order-dependent).
 
     python tools/ts_lib_ab.py main abl/ts_flat.so [--graphs p10m,blog,arxiv] [--reps 4]
 ("main" = the in-tree gwamd/libgraphwalk.so)
+
+Two library instances in one process can differ by up to ~5% on P10M by the
+placement of their tables alone (profiles/r04/ts_lib_ab_three_way.jsonl), so
+--procs N instead runs every library alone in a child process, N rounds in
+alternating order (A B, B A, ...), and reports the median over rounds of
+each process's median launch time.  The parent never touches the GPU.
 """
 import argparse
 import ctypes
@@ -38,7 +44,27 @@ def main():
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--graphs", default="p10m,blog,arxiv")
     ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--procs", type=int, default=0, help="rounds of one child process per library")
     a = ap.parse_args()
+    if a.procs > 0:
+        import subprocess
+        med = {(g, x): [] for g in a.graphs.split(",") for x in a.libs}
+        for rnd in range(a.procs):
+            order = a.libs if rnd % 2 == 0 else list(reversed(a.libs))
+            for x in order:
+                out = subprocess.run([sys.executable, os.path.abspath(__file__), x, "--graphs", a.graphs,
+                                      "--reps", str(a.reps)], check=True, stdout=subprocess.PIPE, text=True).stdout
+                for line in out.splitlines():
+                    d = json.loads(line)
+                    med[(d["graph"], x)].append(d["median_ms"])
+                    print(f"[round {rnd}] {x} {d['graph']}: {d['median_ms']:.3f} ms", file=sys.stderr, flush=True)
+        for g in a.graphs.split(","):
+            base = statistics.median(med[(g, a.libs[0])])
+            for x in a.libs:
+                m = statistics.median(med[(g, x)])
+                print(json.dumps({"graph": g, "lib": x, "median_ms": round(m, 3), "process_medians_ms": med[(g, x)],
+                                  "vs_first": round(m / base, 4), "mode": "separate processes"}), flush=True)
+        return
     import numpy as np
     import torch
     from gwamd import _lib as C
