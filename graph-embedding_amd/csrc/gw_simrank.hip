@@ -124,11 +124,7 @@ __device__ __forceinline__ double seg_scan(double S, int lane, int seg) {
 //   and writes a row total when the next row starts (or the slice ends).
 // Flush: pass 1 writes U[j][i] (column i of U); pass 2 scales by
 // C / (deg_i * deg_j) and writes S'[i][j] and S'[j][i].
-// ATOM: instead of the segmented scan, every lane adds its chunk's 16-term
-// sum to its row's window slot with one LDS f64 atomic (a row's chunks are
-// consecutive lanes / iterations of ONE wave, so the adds of a slot come in a
-// fixed order and the result is deterministic)
-template <bool LDS_ROW, bool PASS2, bool ATOM>
+template <bool LDS_ROW, bool PASS2>
 __global__ void __launch_bounds__(SR_BLOCK) k_sr_gather(SrArgs A, const double* __restrict__ src,
                                                         double* __restrict__ dst, int last, int win) {
   extern __shared__ double lds[];
@@ -146,8 +142,6 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_gather(SrArgs A, const double* 
     if (threadIdx.x == 0) in_row[m] = 0.0;  // the padding entries' slot
   }
   const uint32_t pad_off = (uint32_t)m * 8u;
-  if (ATOM)
-    for (int t = threadIdx.x; t < win; t += SR_BLOCK) out_win[t] = 0.0;  // slots accumulate
   const uint64_t below_incl = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
 
   for (int64_t j0 = PASS2 ? i + 1 : 0; j0 < m; j0 += win) {
@@ -201,15 +195,6 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_gather(SrArgs A, const double* 
           }
           if (!live) p = 0.0;
           if (!live || p0 == 0) fl = 0u;
-          if (ATOM) {
-            const uint64_t hm = __ballot(fl != 0);
-            const int in = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u)) +
-                           (int)fl;
-            if (live) atomicAdd(&out_win[cur_row + in], p);
-            cur_row += __popcll(hm);
-            continue;
-          }
           // heads at or below this lane: v_mbcnt over the head ballot (exclusive
           // count) + this lane's own flag, instead of a 6-step DPP scan
           const uint64_t headmask = __ballot(fl != 0);
@@ -240,7 +225,6 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_gather(SrArgs A, const double* 
     for (int64_t t = threadIdx.x; t < nrow; t += SR_BLOCK) {
       const int64_t j = j0 + t;
       const double val = out_win[t];
-      if (ATOM) out_win[t] = 0.0;  // for the next window (same thread, same slot)
       if (!PASS2) {
         dst[j * m + i] = val;  // U = A S, stored transposed
       } else {
@@ -255,22 +239,14 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_gather(SrArgs A, const double* 
   }
 }
 
-template <bool LDS_ROW, bool PASS2, bool ATOM>
-hipError_t launch_pass_v(const SrArgs& A, const double* src, double* dst, int last, int win, hipStream_t s) {
-  const size_t lds = ((LDS_ROW ? (size_t)A.m + 1 : 0) + (size_t)win) * sizeof(double);
-  hipError_t e = hipFuncSetAttribute((const void*)k_sr_gather<LDS_ROW, PASS2, ATOM>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
-  k_sr_gather<LDS_ROW, PASS2, ATOM><<<(unsigned)A.m, SR_BLOCK, lds, s>>>(A, src, dst, last, win);
-  return hipGetLastError();
-}
-
 template <bool LDS_ROW, bool PASS2>
 hipError_t launch_pass(const SrArgs& A, const double* src, double* dst, int last, int win, hipStream_t s) {
-  // A/B knob (diag library): GW_DIAG_SR_ATOM=1 = the LDS-atomic row reduction
-  const char* at = GW_DIAG_ENV("GW_DIAG_SR_ATOM");
-  if (at && at[0] == '1') return launch_pass_v<LDS_ROW, PASS2, true>(A, src, dst, last, win, s);
-  return launch_pass_v<LDS_ROW, PASS2, false>(A, src, dst, last, win, s);
+  const size_t lds = ((LDS_ROW ? (size_t)A.m + 1 : 0) + (size_t)win) * sizeof(double);
+  hipError_t e = hipFuncSetAttribute((const void*)k_sr_gather<LDS_ROW, PASS2>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  k_sr_gather<LDS_ROW, PASS2><<<(unsigned)A.m, SR_BLOCK, lds, s>>>(A, src, dst, last, win);
+  return hipGetLastError();
 }
 
 template <typename T>

@@ -1339,501 +1339,6 @@ __global__ void __launch_bounds__(TS_BLOCK) k_topsim_pipe_row(TsArgs A) {
   topsim_body<STEP, 0, TS_BLOCK, true>(A);
 }
 
-// ---- streaming kernel (TopSim_singleSample, hash accumulator, top-k rows) --
-// One 1024-thread workgroup per CU holding TWO 6144-slot LDS accumulators
-// (2 x 72 KB) and two level / spawner buffers, so no workgroup barrier
-// separates sources: every wave loops over tasks claimed through LDS
-// counters —
-//   build   the next source's levels into the free slot (one wave, ts_wave_levels),
-//   walk    64 walkers / recorded pair updates of the oldest walkable slot,
-//   output  a slot whose every task is done: top-k by one wave straight from
-//           its LDS accumulator (in-place compaction, radix passes, ranking),
-//           then the accumulator is cleared and the slot freed,
-// so the walker reads of source s+1 run while source s drains and is ranked.
-// A slot's work counter holds (generation << 20 | next task) and its total
-// (generation << 20 | tasks), so a wave whose claim raced with the slot's
-// reuse sees a generation mismatch instead of a task of the new source.
-constexpr int TS_SBLOCK = 1024;
-constexpr int TS_SCO = 1024;  // spawner prefix entries per slot kept in LDS
-constexpr unsigned kSIdxMask = (1u << 20) - 1;
-
-template <int STEP>
-__global__ void __launch_bounds__(TS_SBLOCK) k_topsim_stream(TsArgs A) {
-  constexpr int L = 2 * STEP;
-  constexpr int NW = TS_SBLOCK / 64;
-  using H = TsHash<2>;
-  constexpr int HS = H::SLOTS;
-  constexpr int HL = H::LIMIT;
-  extern __shared__ double s_dyn[];  // [2][HS] values, then [2][HS] keys
-  __shared__ int32_t s_co[2][TS_SCO];
-  __shared__ unsigned s_hist[256];
-  __shared__ double s_selv[TOPK_MAX];
-  __shared__ int32_t s_seli[TOPK_MAX];
-  __shared__ TsPipeMeta s_pm[2];
-  __shared__ unsigned s_deal[2], s_totgen[2], s_seq[2];
-  __shared__ int s_done[2], s_state[2], s_hcount[2], s_ntouch[2];  // state: 0 free, 1 building, 2 walkable, 3 output
-  __shared__ int s_building, s_outbusy, s_end, s_bslot;
-  __shared__ unsigned s_gen;
-  __shared__ long long s_red[NW];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int64_t blk = blockIdx.x;
-  const gw_dev_graph& G = A.G;
-  const int64_t cap = A.level_cap;
-  const int64_t lvl_stride = (int64_t)(L + 1) * cap;
-  const uint32_t ov_mask = (uint32_t)(A.touch_cap - 1);
-  int32_t* const hk_all = reinterpret_cast<int32_t*>(s_dyn + 2 * HS);
-
-  for (int j = tid; j < 2 * HS; j += TS_SBLOCK) {
-    s_dyn[j] = 0.0;
-    hk_all[j] = -1;
-  }
-  if (tid == 0) {
-    for (int b = 0; b < 2; ++b) {
-      s_deal[b] = 0u;
-      s_totgen[b] = 0u;
-      s_seq[b] = 0u;
-      s_done[b] = 0;
-      s_state[b] = 0;
-      s_hcount[b] = 0;
-      s_ntouch[b] = 0;
-    }
-    s_building = 0;
-    s_outbusy = 0;
-    s_end = 0;
-    s_bslot = 0;
-    s_gen = 1u;
-  }
-  __syncthreads();
-
-  long long my_ext = 0, my_upd = 0, my_walk = 0, my_maxf = 0;
-  auto ld = [](const int* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); };
-  auto ldu = [](const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); };
-  auto st = [](int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); };
-
-  auto ov_add = [&](int b, int32_t target, double val) {
-    int32_t* ov_key = A.ov_keys + (blk * 2 + b) * A.touch_cap;
-    double* ov_val = A.ov_vals + (blk * 2 + b) * A.touch_cap;
-    int32_t* touched = A.touched + (blk * 2 + b) * A.touch_cap;
-    uint32_t h = ((uint32_t)target * 0x9E3779B1u) & ov_mask;
-    for (int64_t probe = 0; probe <= (int64_t)ov_mask; ++probe) {
-      const int32_t old = atomicCAS(&ov_key[h], -1, target);
-      if (old == -1 || old == target) {
-        if (old == -1) {
-          const int k = atomicAdd(&s_ntouch[b], 1);
-          if ((int64_t)k < A.touch_cap * 3 / 4) touched[k] = (int32_t)h;
-          else atomicOr(A.error_flag, 2);
-        }
-        atomicAdd(&ov_val[h], val);
-        return;
-      }
-      h = (h + 1) & ov_mask;
-    }
-    atomicOr(A.error_flag, 2);
-  };
-  auto add = [&](int b, int32_t target, double val) {
-    double* hv = s_dyn + b * HS;
-    int32_t* hk = hk_all + b * HS;
-    uint32_t h = H::slot(target);
-    for (int probe = 0; probe < HS; ++probe) {
-      const int32_t k = hk[h];
-      if (k == target) {
-        atomicAdd(&hv[h], val);
-        return;
-      }
-      if (k == -1) {
-        if (atomicAdd(&s_hcount[b], 1) >= HL) break;
-        const int32_t old = atomicCAS(&hk[h], -1, target);
-        if (old == -1 || old == target) {
-          atomicAdd(&hv[h], val);
-          return;
-        }
-      }
-      h = H::next(h);
-    }
-    ov_add(b, target, val);
-  };
-  // one walker (index g in the reference's queue order) of slot b's source
-  auto run_walker = [&](int g, int b, int32_t s, int ds, int ns) {
-    const int32_t* Vb = A.lvl_vertex + (blk * 2 + b) * lvl_stride;
-    const int32_t* Db = A.lvl_deg + (blk * 2 + b) * lvl_stride;
-    const int32_t* Pb = A.lvl_parent + (blk * 2 + b) * lvl_stride;
-    const int64_t* Ob = A.lvl_off + (blk * 2 + b) * lvl_stride;
-    const int32_t* SFb = A.spawn_first + (blk * 2 + b) * (A.spawn_cap + 1);
-    const int sp = upper_bound_i32(ns + 1 <= TS_SCO ? s_co[b] : SFb, ns + 1, g) - 1;
-    const int64_t sb = (blk * 2 + b) * A.spawn_cap + sp;
-    const int l0 = A.spawn_level[sb];
-    const double mw = A.spawn_mass[sb];
-    int32_t path[L + 1], dpath[L + 1];
-    int p = A.spawn_node[sb];
-    int32_t dcur = ds;
-    int64_t ocur = l0 == 0 ? Ob[0] : Ob[(int64_t)l0 * cap + p];
-#pragma unroll
-    for (int t = L; t >= 1; --t) {
-      if (t <= l0) {
-        path[t] = Vb[(int64_t)t * cap + p];
-        dpath[t] = Db[(int64_t)t * cap + p];
-        p = Pb[(int64_t)t * cap + p];
-      }
-    }
-    path[0] = s;
-    dpath[0] = ds;
-#pragma unroll
-    for (int t = 0; t <= L; ++t)
-      if (t == l0) dcur = dpath[t];
-    bool alive = true;
-#pragma unroll
-    for (int t = 1; t <= L; ++t) {
-      if (t > l0 && alive) {
-        if (dcur == 0) {
-          alive = false;
-        } else {
-          const gw_u4 u = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)t, 0u, A.k0, A.k1);
-          const uint64_t ei = (uint64_t)ocur + gw_index(u.x, u.y, (uint32_t)dcur);
-          const gw_ts_ent e = gw_ts_load(A.ent + ei);  // randNeighbor
-          path[t] = e.x;
-          dpath[t] = e.d;
-          dcur = e.d;
-          ocur = e.off;
-          ++my_ext;
-          if ((t & 1) == 0) {  // computePathSim at pathLen = t (TopSim_singleSample.java:157, 183-189)
-            const int i = t / 2;
-            bool meet = path[t] != s;
-#pragma unroll
-            for (int q = 0; q < STEP; ++q)  // isFirstMeet (:211-218)
-              if (q < i && path[q] == path[t - q]) meet = false;
-            if (meet) {
-              add(b, path[t], ((mw * A.cache[i]) * (double)dpath[i]) / (double)dpath[t]);
-              ++my_upd;
-            }
-          }
-        }
-      }
-    }
-    ++my_walk;
-  };
-  // top-k of slot b's finished source by this wave, then the slot is freed
-  auto output = [&](int b) {
-    int lane = tid & 63;
-    asm volatile("" : "+v"(lane));  // per-lane LDS addresses formed here, not held across the task loop
-    double* hv = s_dyn + b * HS;
-    int32_t* hk = hk_all + b * HS;
-    int32_t* ov_key = A.ov_keys + (blk * 2 + b) * A.touch_cap;
-    double* ov_val = A.ov_vals + (blk * 2 + b) * A.touch_cap;
-    const int32_t* touched = A.touched + (blk * 2 + b) * A.touch_cap;
-    const int64_t r = s_pm[b].r;
-    const int K = A.topk;
-    const int nov = (int)min((int64_t)ld(&s_ntouch[b]), A.touch_cap * 3 / 4);
-    // overflow keys that also reached the LDS table fold into their LDS entry
-    for (int k = lane; k < nov; k += 64) {
-      const int32_t slot = touched[k];
-      const int32_t key = __hip_atomic_load(&ov_key[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint32_t h = H::slot(key);
-      for (int probe = 0; probe < HS; ++probe) {
-        const int32_t kk = hk[h];
-        if (kk == -1) break;
-        if (kk == key) {
-          atomicAdd(&hv[h], __hip_atomic_load(&ov_val[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          __hip_atomic_store(&ov_val[slot], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        h = H::next(h);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    // in-place compaction of the occupied slots to [0, NL) (writes never pass the chunk being read)
-    constexpr int UC = 8;
-    static_assert(HS % (64 * UC) == 0, "compaction chunks");
-    int NL = 0;
-    for (int c0 = 0; c0 < HS; c0 += 64 * UC) {
-      int32_t kk[UC];
-      double vv[UC];
-#pragma unroll
-      for (int u = 0; u < UC; ++u) {
-        kk[u] = hk[c0 + u * 64 + lane];
-        vv[u] = hv[c0 + u * 64 + lane];
-      }
-#pragma unroll
-      for (int u = 0; u < UC; ++u)
-        if (kk[u] != -1) {
-          hk[c0 + u * 64 + lane] = -1;
-          hv[c0 + u * 64 + lane] = 0.0;
-        }
-#pragma unroll
-      for (int u = 0; u < UC; ++u) {
-        const unsigned long long m = __ballot(kk[u] != -1);
-        const int pos = NL + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (kk[u] != -1) {
-          hk[pos] = kk[u];
-          hv[pos] = vv[u];
-        }
-        NL += __popcll(m);
-      }
-    }
-    const int NC = NL + nov;
-    auto cval = [&](int idx) -> double {
-      return idx < NL ? hv[idx]
-                      : __hip_atomic_load(&ov_val[touched[idx - NL]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    auto cid = [&](int idx) -> int32_t {
-      return idx < NL ? hk[idx]
-                      : __hip_atomic_load(&ov_key[touched[idx - NL]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    auto count = [&](bool in, int dg) {
-      const unsigned long long act = __ballot(in);
-      if (!act) return;
-      const int f = __ffsll(act) - 1;
-      const int d0 = __builtin_amdgcn_readlane(dg, f);
-      if (__ballot(in && dg == d0) == act) {
-        if (lane == f) atomicAdd(&s_hist[d0], (unsigned)__popcll(act));
-      } else if (in) {
-        atomicAdd(&s_hist[dg], 1u);
-      }
-    };
-    // radix select of the K-th largest key (value bits), 8 bits a pass
-    unsigned long long pre = 0, msk = 0;
-    int need = K;
-    bool take_all = false, exact = false;
-    for (int shift = 56; shift >= 0; shift -= 8) {
-      {
-        unsigned z = 0u;
-        asm volatile("" : "+v"(z));  // (a zero vector held across the task loop spilled)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) s_hist[4 * lane + q] = z;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      for (int i0 = 0; i0 < NC; i0 += 64 * UC) {
-        double v[UC];
-#pragma unroll
-        for (int u = 0; u < UC; ++u) {
-          const int i = i0 + u * 64 + lane;
-          v[u] = i < NC ? cval(i) : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < UC; ++u) {
-          const unsigned long long k = dkey(v[u]);
-          count(v[u] > 0.0 && (k & msk) == pre, (int)((k >> shift) & 255));
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      int bin, before, total;
-      select_bin_w(s_hist, need, true, bin, before, total);
-      if (shift == 56 && total <= K) {
-        take_all = true;
-        break;
-      }
-      const int inbin = (int)s_hist[bin];
-      need -= before;
-      pre |= (unsigned long long)bin << shift;
-      msk |= 255ull << shift;
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      if (inbin == need) {  // the K-th key's bin is taken whole
-        exact = true;
-        break;
-      }
-    }
-    int32_t idT = 0x7fffffff;  // ties at the threshold: smallest ids first
-    if (!take_all && !exact) {
-      unsigned ipre = 0u, imsk = 0u;
-      for (int shift = 24; shift >= 0; shift -= 8) {
-        {
-          unsigned z = 0u;
-          asm volatile("" : "+v"(z));
-#pragma unroll
-          for (int q = 0; q < 4; ++q) s_hist[4 * lane + q] = z;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        for (int i = lane; i < NC; i += 64) {
-          const bool eq = dkey(cval(i)) == pre;
-          const unsigned id = eq ? (unsigned)cid(i) : 0u;
-          count(eq && (id & imsk) == ipre, (int)((id >> shift) & 255));
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        int bin, before, total;
-        select_bin_w(s_hist, need, false, bin, before, total);
-        need -= before;
-        ipre |= (unsigned)bin << shift;
-        imsk |= 255u << shift;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      }
-      idT = (int32_t)ipre;
-    }
-    // collect (<= K) and rank
-    int cnt = 0;
-    for (int i0 = 0; i0 < NC; i0 += 64) {
-      const int i = i0 + lane;
-      double v = 0.0;
-      int32_t id = 0;
-      bool sel = false;
-      if (i < NC) {
-        v = cval(i);
-        if (v > 0.0) {
-          id = cid(i);
-          const unsigned long long k = dkey(v);
-          sel = take_all || (exact ? (k & msk) >= pre : (k > pre || (k == pre && id <= idT)));
-        }
-      }
-      const unsigned long long sm = __ballot(sel);
-      const int slot = cnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-      if (sel && slot < TOPK_MAX) {
-        s_seli[slot] = id;
-        s_selv[slot] = v;
-      }
-      cnt += __popcll(sm);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    ts_wave_rank(s_seli, s_selv, min(cnt, TOPK_MAX), K, A.out_ids + r * (int64_t)K, A.out_scores + r * (int64_t)K);
-    // clear the accumulator, free the slot
-    for (int j = lane; j < NL; j += 64) {
-      hv[j] = 0.0;
-      hk[j] = -1;
-    }
-    for (int k = lane; k < nov; k += 64) {
-      const int32_t slot = touched[k];
-      __hip_atomic_store(&ov_key[slot], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ov_val[slot], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __threadfence_block();
-    if (lane == 0) {
-      s_hcount[b] = 0;
-      s_ntouch[b] = 0;
-      st(&s_state[b], 0);
-      st(&s_outbusy, 0);
-    }
-  };
-
-  unsigned spins = 0;
-  for (;;) {
-    int task = 0, tb = 0;
-    unsigned tidx = 0;
-    if (lane == 0) {
-      // output: a walkable slot whose every task is done (one output at a time)
-      for (int b = 0; b < 2 && !task; ++b) {
-        if (ld(&s_state[b]) != 2) continue;
-        const unsigned tg = ldu(&s_totgen[b]);
-        if ((unsigned)ld(&s_done[b]) < (tg & kSIdxMask)) continue;
-        if (atomicCAS(&s_outbusy, 0, 1) != 0) break;
-        if (atomicCAS(&s_state[b], 2, 3) == 2) {
-          task = 1;
-          tb = b;
-        } else {
-          st(&s_outbusy, 0);
-        }
-      }
-      // build: the next slot, once free
-      if (!task && !ld(&s_end)) {
-        const int nb = ld(&s_bslot);
-        if (ld(&s_state[nb]) == 0 && atomicCAS(&s_building, 0, 1) == 0) {
-          if (ld(&s_state[nb]) == 0 && ld(&s_bslot) == nb) {
-            st(&s_state[nb], 1);
-            task = 2;
-            tb = nb;
-          } else {
-            st(&s_building, 0);
-          }
-        }
-      }
-      // walk: the oldest walkable slot with tasks left
-      if (!task) {
-        const bool swap = ld(&s_state[1]) == 2 && (ld(&s_state[0]) != 2 || (int)(ldu(&s_seq[1]) - ldu(&s_seq[0])) < 0);
-        for (int q = 0; q < 2 && !task; ++q) {
-          const int b = swap ? 1 - q : q;
-          if (ld(&s_state[b]) != 2) continue;
-          const unsigned tg = ldu(&s_totgen[b]);
-          const unsigned d = ldu(&s_deal[b]);
-          if ((d >> 20) != (tg >> 20) || (d & kSIdxMask) >= (tg & kSIdxMask)) continue;
-          const unsigned v = atomicAdd(&s_deal[b], 64u);
-          const unsigned tg2 = ldu(&s_totgen[b]);
-          if ((v >> 20) == (tg2 >> 20) && (v & kSIdxMask) < (tg2 & kSIdxMask)) {
-            task = 3;
-            tb = b;
-            tidx = v & kSIdxMask;
-          }
-        }
-      }
-      if (!task && ld(&s_end) && ld(&s_state[0]) == 0 && ld(&s_state[1]) == 0 && ld(&s_building) == 0) task = 4;
-    }
-    task = __shfl(task, 0, 64);
-    tb = __shfl(tb, 0, 64);
-    tidx = (unsigned)__shfl((int)tidx, 0, 64);
-    if (task == 4) break;
-    if (task == 0) {
-      if (++spins > (1u << 22)) {  // a wait no schedule reaches: flag it and leave
-        if (lane == 0) atomicOr(A.error_flag, 8);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    spins = 0;
-    if (task == 3) {
-      const int nw = s_pm[tb].nwalk, ne = s_pm[tb].ncontrib;
-      const int g = (int)tidx + lane;
-      if (g < nw) {
-        run_walker(g, tb, s_pm[tb].s, s_pm[tb].ds, s_pm[tb].nspawn);
-      } else if (g < nw + ne) {
-        const int64_t eb = (blk * 2 + tb) * A.enum_cap;
-        add(tb, A.enum_tgt[eb + g - nw], A.enum_val[eb + g - nw]);
-      }
-      __threadfence_block();  // accumulator / overflow adds before the done count
-      if (lane == 0) atomicAdd(&s_done[tb], min(64, nw + ne - (int)tidx));
-    } else if (task == 1) {
-      output(tb);
-    } else {  // build
-      long long r = 0;
-      if (lane == 0) r = (long long)atomicAdd(A.src_counter, 1u);
-      r = ((long long)__shfl((int)(r >> 32), 0, 64) << 32) | (uint32_t)__shfl((int)r, 0, 64);
-      if (r >= A.nsrc) {
-        if (lane == 0) {
-          st(&s_end, 1);
-          st(&s_state[tb], 0);
-          st(&s_building, 0);
-        }
-        continue;
-      }
-      const TsLevelStats ls = ts_wave_levels<STEP>(A, tb, (int64_t)r, s_pm);
-      my_ext += ls.ext;
-      my_upd += ls.upd;
-      if (ls.maxf > my_maxf) my_maxf = ls.maxf;
-      __threadfence_block();
-      const int ns = s_pm[tb].nspawn;
-      if (ns + 1 <= TS_SCO) {
-        const int32_t* SFb = A.spawn_first + (blk * 2 + tb) * (A.spawn_cap + 1);
-        for (int k = lane; k <= ns; k += 64) s_co[tb][k] = SFb[k];
-      }
-      __threadfence_block();
-      if (lane == 0) {
-        const unsigned gen = s_gen & 0xFFFu;
-        s_gen = s_gen + 1u;
-        s_seq[tb] = s_gen;
-        s_done[tb] = 0;
-        __hip_atomic_store(&s_totgen[tb], (gen << 20) | (unsigned)(s_pm[tb].nwalk + s_pm[tb].ncontrib),
-                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        atomicExch(&s_deal[tb], gen << 20);
-        st(&s_state[tb], 2);
-        st(&s_bslot, 1 - tb);
-        st(&s_building, 0);
-      }
-    }
-  }
-
-  // statistics
-  long long e = block_sum<long long, NW>(my_ext, s_red);
-  long long u = block_sum<long long, NW>(my_upd, s_red);
-  long long w = block_sum<long long, NW>(my_walk, s_red);
-  long long mf = my_maxf;  // the builder may be any wave
-  for (int o = 32; o > 0; o >>= 1) mf = max(mf, (long long)__shfl_down(mf, o, 64));
-  if (lane == 0 && mf > 0 && A.stats) atomicMax(&A.stats[2], mf);
-  if (tid == 0 && A.stats) {
-    atomicAdd((unsigned long long*)&A.stats[0], (unsigned long long)e);
-    atomicAdd((unsigned long long*)&A.stats[1], (unsigned long long)u);
-    atomicAdd((unsigned long long*)&A.stats[3], (unsigned long long)w);
-  }
-}
-
 template <typename T>
 int ws_alloc(gw_graph* g, T** p, int64_t count) {
   *p = nullptr;
@@ -1885,13 +1390,6 @@ hipError_t launch_mode(int mode, bool pipe, const TsArgs& A, int blocks, size_t 
                                        (int)lds);
     if (e != hipSuccess) return e;
     k_topsim_pipe<STEP><<<blocks, TS_BLOCK, lds, s>>>(A);
-    return hipGetLastError();
-  }
-  if (mode == 3) {  // streaming kernel (pipe workspace, two accumulators per workgroup)
-    hipError_t e = hipFuncSetAttribute((const void*)k_topsim_stream<STEP>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    k_topsim_stream<STEP><<<blocks, TS_SBLOCK, lds, s>>>(A);
     return hipGetLastError();
   }
   if (mode == 0 && pipe) {
@@ -2008,23 +1506,17 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
               ((mode == 2 && sample <= kPipeMaxSample) || (mode == 0 && (size_t)n * 8 > TS_2WG_LDS));
   if (const char* np = GW_DIAG_ENV("GW_DIAG_TS_NOPIPE"))  // A/B knob: the unpipelined kernel
     if (np[0] == '1') pipe = false;
-  // experiment (diag library): the streaming kernel, one 1024-thread
-  // workgroup per CU with two accumulators (top-k rows only)
-  bool stream = false;
-  if (const char* ss = GW_DIAG_ENV("GW_DIAG_TS_STREAM"))
-    if (ss[0] == '1' && pipe && mode == 2) stream = true;
-  const int64_t ovb = stream ? 2 : 1;  // overflow tables per workgroup
   const int64_t nb = pipe ? 2 : 1;
   const int64_t enum_cap = pipe ? (int64_t)step * level_cap : 1;
   const int64_t per_block = nb * ((int64_t)(L + 1) * level_cap * 20 + spawn_cap * 20 + 4) + 2 * level_cap * 8 +
                             (level_cap + 1) * 4 + (pipe ? 2 * enum_cap * 12 : 0) +
-                            (lds_row ? 0 : ovb * touch_cap * 16) + (pipe ? TOPK_MAX * 12 : 0);
+                            (lds_row ? 0 : touch_cap * 16) + (pipe ? TOPK_MAX * 12 : 0);
   int dev_cus = 256;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, g->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
   const int64_t budget = (int64_t)16 << 30;  // 16 GB of the 288 GB HBM
   int64_t blocks = std::min<int64_t>(4 * dev_cus, budget / std::max<int64_t>(per_block, 1));  // persistent
-  if (variant == GW_TOPSIM_ENUMERATE || stream) blocks = std::min<int64_t>(blocks, dev_cus);
+  if (variant == GW_TOPSIM_ENUMERATE) blocks = std::min<int64_t>(blocks, dev_cus);
   if (blocks < 1) {
     g->err = "TopSim workspace exceeds the 16 GB budget";
     return GW_ERR_CAPACITY;
@@ -2042,7 +1534,7 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
       (rc = ws_alloc(g, &t.spawn_mass, blocks * nb * spawn_cap)) ||
       (rc = ws_alloc(g, &t.enum_tgt, blocks * 2 * enum_cap)) ||
       (rc = ws_alloc(g, &t.enum_val, blocks * 2 * enum_cap)) ||
-      (rc = ws_alloc(g, &t.touched, ovb * blocks * touch_cap)) ||
+      (rc = ws_alloc(g, &t.touched, blocks * touch_cap)) ||
       (rc = ws_alloc(g, &t.dsel_id, pipe ? blocks * TOPK_MAX : 1)) ||
       (rc = ws_alloc(g, &t.dsel_val, pipe ? blocks * TOPK_MAX : 1)) ||
       (rc = ws_alloc(g, &t.src_counter, 1)) || (rc = ws_alloc(g, &t.error_flag, 1)))
@@ -2053,11 +1545,10 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
     GW_HIP_TRY(hipGetLastError());
   }
   if (!lds_row) {
-    if ((rc = ws_alloc(g, &t.acc_row, ovb * blocks * touch_cap)) ||
-        (rc = ws_alloc(g, &t.ov_keys, ovb * blocks * touch_cap)))
+    if ((rc = ws_alloc(g, &t.acc_row, blocks * touch_cap)) || (rc = ws_alloc(g, &t.ov_keys, blocks * touch_cap)))
       return rc;
-    GW_HIP_TRY(hipMemset(t.acc_row, 0, sizeof(double) * ovb * blocks * touch_cap));
-    GW_HIP_TRY(hipMemset(t.ov_keys, 0xFF, sizeof(int32_t) * ovb * blocks * touch_cap));  // -1 = empty
+    GW_HIP_TRY(hipMemset(t.acc_row, 0, sizeof(double) * blocks * touch_cap));
+    GW_HIP_TRY(hipMemset(t.ov_keys, 0xFF, sizeof(int32_t) * blocks * touch_cap));  // -1 = empty
   }
   t.variant = variant;
   t.sample = sample;
@@ -2067,11 +1558,10 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   t.level_cap = level_cap;
   t.spawn_cap = spawn_cap;
   t.touch_cap = touch_cap;
-  t.lds_row = stream ? 3 : mode;
+  t.lds_row = mode;
   t.pipe = pipe ? 1 : 0;
   t.enum_cap = enum_cap;
   t.lds_bytes = lds_row ? (size_t)n * 8 : (size_t)(mode == 2 ? TsHash<2>::SLOTS : TsHash<1>::SLOTS) * 12;
-  if (stream) t.lds_bytes = (size_t)2 * TsHash<2>::SLOTS * 12;
   GW_HIP_TRY(hipDeviceSynchronize());
   return GW_OK;
 }
@@ -2144,12 +1634,7 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
     GW_HIP_TRY(hipMalloc((void**)&A.phase, 10 * sizeof(unsigned long long)));
     GW_HIP_TRY(hipMemsetAsync(A.phase, 0, 10 * sizeof(unsigned long long), s));
   }
-  // the streaming kernel writes top-k rows only; dense / sparse rows run the
-  // pipelined kernel on the same workspace (a superset of its own)
-  const bool rows_too = out_rows_dev || sparse || !out_ids_dev;
-  const int kmode = t.lds_row == 3 && rows_too ? 2 : t.lds_row;
-  const size_t klds = t.lds_row == 3 && rows_too ? (size_t)TsHash<2>::SLOTS * 12 : t.lds_bytes;
-  hipError_t e = launch(step, kmode, t.pipe != 0, A, blocks, klds, s);
+  hipError_t e = launch(step, t.lds_row, t.pipe != 0, A, blocks, t.lds_bytes, s);
   if (e != hipSuccess) {
     g->err = std::string("k_topsim launch: ") + hipGetErrorString(e);
     return GW_ERR_DEVICE;
@@ -2173,10 +1658,6 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   if (flag & 4) {
     g->err = "sparse rows exceed the output capacity (rows with len -1 did not fit; *used = room needed)";
     return GW_ERR_CAPACITY;
-  }
-  if (flag & 8) {
-    g->err = "streaming TopSim kernel: a wave waited past its limit (task schedule stalled)";
-    return GW_ERR_DEVICE;
   }
   return GW_OK;
 }

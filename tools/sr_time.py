@@ -1,7 +1,7 @@
 """Time naive SimRank (SimRank.java) on the GPU: blog / moreno / g333.
 
     python tools/sr_time.py [blog moreno ...]
-    python tools/sr_time.py --knob GW_DIAG_SR_ATOM --modes 0,1 --reps 5 blog
+    python tools/sr_time.py --knob GW_DIAG_<KNOB> --modes 0,1 --reps 5 blog
         (diag library: the knob's values alternate in one process, 3 rounds each,
         and every mode's result is compared with the first mode's)
 """
