@@ -710,6 +710,11 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     for (int t = 0; t <= L; ++t)
       if (t == l0) dcur = dpath[t];
     bool alive = true;
+    // the draw of step t depends on (s, g, t) only: step t+1's Philox block is
+    // computed while step t's entry load is in flight, off the dependent chain
+    const bool hoist = !(kGwDiag && (A.diag & 128));  // diag bit 128: draw after the load (A/B)
+    gw_u4 un = {0u, 0u, 0u, 0u};
+    if (hoist) un = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)(l0 + 1), 0u, A.k0, A.k1);
 #pragma unroll
     for (int t = 1; t <= L; ++t) {
       if (t > l0 && alive) {
@@ -721,6 +726,9 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
             ux = ((uint32_t)s * 0x9E3779B1u) ^ ((uint32_t)g * 0x85EBCA6Bu) ^ ((uint32_t)t * 0xC2B2AE35u);
             ux ^= ux >> 15;
             ux *= 0x2C1B3C6Du;
+          } else if (hoist) {
+            ux = un.x;
+            uy = un.y;
           } else {
             const gw_u4 u = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)t, 0u, A.k0, A.k1);
             ux = u.x;
@@ -730,6 +738,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           if (kGwDiag && (A.diag & 12))  // timing only: walker reads confined to 1 GB / 2 GB of the table
             ei &= (A.diag & 4) ? ((1ull << 26) - 1) : ((1ull << 27) - 1);
           const gw_ts_ent e = gw_ts_load(A.ent + ei);  // randNeighbor
+          if (hoist && t < L) un = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)(t + 1), 0u, A.k0, A.k1);
           path[t] = e.x;
           dpath[t] = e.d;
           dcur = e.d;
