@@ -617,6 +617,18 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       return;
     }
     uint32_t h = H::slot(target);
+    if (kGwDiag && (A.diag & 512)) {  // experiment: no shared load counter, a probe-length cap instead
+      for (int probe = 0; probe < 64; ++probe) {
+        const int32_t k = s_hkey[h];
+        if (k == target || (k == -1 && (atomicCAS(&s_hkey[h], -1, target) == -1 || s_hkey[h] == target))) {
+          atomicAdd(&s_hval[h], val);
+          return;
+        }
+        h = H::next(h);
+      }
+      ov_add(target, val);
+      return;
+    }
     for (int probe = 0; probe < HASH_SLOTS; ++probe) {
       const int32_t k = s_hkey[h];
       if (k == target) {
