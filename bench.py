@@ -101,6 +101,8 @@ def parse(argv):
     ap.add_argument("--simrank-rounds", type=int, default=3, help="SimRank.java STEP")
     ap.add_argument("--no-rmat24", action="store_true", help="skip config 4 as a secondary")
     ap.add_argument("--no-p10m", action="store_true", help="skip config 5 as a secondary")
+    ap.add_argument("--no-p10m-stretch", action="store_true",
+                    help="skip config 5's stretch (SAMPLE 10000, STEP 5) as a secondary")
     ap.add_argument("--no-arxiv", action="store_true",
                     help="skip the arxiv line (same graph as the reference CPU fixture)")
     ap.add_argument("--secondary", choices=["auto", "all", "none"], default="auto",
@@ -671,11 +673,33 @@ def walk_headline(R, args):
                                                        "at q > 1, no per-edge tables)")
         alt["walk_steps_per_s"] = launch_steps / rw
         alt["trials_per_step"] = int(cnt[1].item()) / max(int(cnt[0].item()), 1)
+        rname = walk_kernel_name("rejection", G)
+        alt["roofline"] = walk_roofline(
+            rname, f"n2v_rmat{args.scale}_ef{args.edge_factor}_p{args.p}_q{args.q}_L{L}_r{args.num_walks}_rejection",
+            int(cnt[0].item()), rw, max(G.info().sampler_bytes, 16 * nnz), grid_threads(cnt_w))
         res["end_to_end_rejection"] = alt
         res["end_to_end_best"] = "bitset" if res["end_to_end"]["total_s"] <= alt["total_s"] else "rejection"
     del out
     G.free()
     return res
+
+
+def walk_roofline(kname, tag, steps, kernel_s, table_bytes, grid):
+    """36 B per walk-step over one launch's event time, with the
+    PMC traffic / fabric requests of this library build when
+    profiles/pmc_summary.json holds an entry keyed to it (pmc_tag +
+    lib_sha256 + steps per launch)."""
+    prof = load_prof(tag, steps)
+    achieved = BYTES_PER_STEP * steps / kernel_s / 1e9
+    line = line_roofline(prof, kernel_s, table_bytes)
+    line["ceiling_frac_at_one_request_per_step"] = \
+        BYTES_PER_STEP * line["calibrated_peak_lines_per_s"] / (HBM_PEAK_GBS * 1e9)
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": prof["hbm_bytes_per_launch"] if prof else None,
+            "traffic_note": (prof or {}).get("note"), "kernel": kname, "kernel_ms": kernel_s * 1e3,
+            "bytes_per_unit": BYTES_PER_STEP, "units_per_launch": steps, "pmc_tag": tag,
+            "pmc_match": {"kernel": kname, "grid": grid}, "lib_sha256": lib_digest(),
+            "random_line_roofline": line}
 
 
 def end_to_end(prep_s, launch_s, launch_steps, launches, what):
@@ -824,6 +848,10 @@ def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejectio
                              f"prepare + {baseline_r} walks from every vertex, rejection sampler")
         e2e_rej["walk_steps_per_s"] = rsteps / rw
         e2e_rej["trials_per_step"] = int(rcnt[1].item()) / max(rsteps, 1)
+        rname = walk_kernel_name("rejection", BG)
+        e2e_rej["roofline"] = walk_roofline(
+            rname, f"n2v_rmat{scale}_ef{ef}_p{wp}_q{wq}_L{L}_r{walks_per_node}_rejection", rsteps, rw,
+            max(BG.info().sampler_bytes, 16 * bi.nnz), grid_threads(nb))
         e2e_best = "bitset" if e2e["total_s"] <= e2e_rej["total_s"] else "rejection"
         del rout
         BG.options(listed=-1)
@@ -879,9 +907,29 @@ def topsim_roofline(ext, upd, kt, tag, nsrc, nnz, step):
             "random_line_roofline": line_roofline(prof, kt, table, 128)}
 
 
-def run_topsim(R, args, name):
+_P10M_GRAPH = {}  # the P10M graph built once per run (config 5 and its SAMPLE 10000 / STEP 5 stretch)
+
+
+def p10m_graph(R, args):
+    import numpy as np
+    import gwamd
+    key = (args.p10m_vertices, args.seed, args.rmat_params)
+    if key not in _P10M_GRAPH:
+        t0 = time.perf_counter()
+        a, b, c = rmat_abc(args)
+        pg = gwamd.GWGraph.rmat_java(args.p10m_vertices, 10 * args.p10m_vertices, a, b, c, args.seed)
+        csr = pg.export_csr()
+        log(f"[rank {R.rank}] p10m built in {time.perf_counter() - t0:.1f}s")
+        pg.to_device(R.dev.index)
+        _P10M_GRAPH.clear()
+        _P10M_GRAPH[key] = (pg, csr["offsets"], csr["nbrs"], np.diff(csr["offsets"]))
+    return _P10M_GRAPH[key]
+
+
+def run_topsim(R, args, name, sample=None, step=None):
     """TopSim_singleSample: lshrank graphs (config 3; every rank all sources) or
-    P10M (config 5; sources split over ranks, strong scaling)."""
+    P10M (config 5 at SAMPLE 1000 / STEP 3, or the SURVEY §8d stretch
+    SAMPLE 10000 / STEP 5; sources split over ranks, strong scaling)."""
     import numpy as np
     torch = R.torch
     import gwamd
@@ -911,14 +959,7 @@ def run_topsim(R, args, name):
     if name == "p10m":
         # config 5: 10M-vertex Java-semantics R-MAT (reference quadrant recursion),
         # 1e8 generated lines, all non-isolated sources, top-100
-        t0 = time.perf_counter()
-        a, b, c = rmat_abc(args)
-        pg = gwamd.GWGraph.rmat_java(args.p10m_vertices, 10 * args.p10m_vertices, a, b, c, args.seed)
-        csr = pg.export_csr()
-        offs, nbrs = csr["offsets"], csr["nbrs"]
-        deg = np.diff(offs)
-        log(f"[rank {rank}] p10m built in {time.perf_counter() - t0:.1f}s")
-        pg.to_device(R.dev.index)
+        pg, offs, nbrs, deg = p10m_graph(R, args)
         h = pg.handle
         srcs_all = np.nonzero(deg > 0)[0].astype(np.int32)
         # round-robin split: R-MAT puts the hubs (the expensive sources) at low
@@ -927,7 +968,7 @@ def run_topsim(R, args, name):
         srcs = srcs_all[rank::world]
         desc = (f"{args.p10m_vertices} vertices, {10 * args.p10m_vertices} R-MAT lines, {len(srcs_all)} non-isolated "
                 f"sources split round-robin over {world} rank(s)")
-        K, sample, step = 100, 1000, 3
+        K, sample, step = 100, sample or 1000, step or 3
         scaling = "strong"
         keep = pg
     else:
@@ -991,6 +1032,8 @@ def run_topsim(R, args, name):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu_ts = cpu_baseline_topsim(offs, nbrs, len(offs) - 1, sample, step, args.seed,
                                      args.cpu_seconds if name != "p10m" else 15.0, sources=srcs, topk=K)
+    if name == "p10m":
+        desc += f", SAMPLE {sample}, STEP {step}" + (" (SURVEY §8d stretch)" if (sample, step) != (1000, 3) else "")
     del keep
     return {
         "metric": "SimRank pair-updates/sec (TopSim_singleSample)", "value": upd / tel,
@@ -1184,6 +1227,8 @@ def main(argv):
             BG.free()
         if not args.no_p10m:
             secondary["topsim_p10m"] = run_topsim(R, args, "p10m")
+        if not args.no_p10m_stretch:
+            secondary["topsim_p10m_stretch"] = run_topsim(R, args, "p10m", 10000, 5)
     if R.rank == 0:
         ngpu = R.ngpu
         res = {

@@ -234,7 +234,7 @@ int gw_graph_info(const gw_graph* g, gw_graph_info_t* info) {
   info->device = g->device;
   info->sampler_bytes = (g->d.bs_nbr ? g->bitset_words * 4 + g->nnz * (int64_t)sizeof(gw_bs_nbr) : 0) +
                         (g->d.sent ? g->nnz * (int64_t)sizeof(gw_ts_ent) : 0) +
-                        (g->d.eh ? 2 * g->nnz * (int64_t)sizeof(int32_t) : 0);
+                        (g->d.eh ? 4 * g->nnz * (int64_t)sizeof(int32_t) : 0);
   info->n2v_mode = g->n2v_prepared ? g->n2v_mode : -1;
   info->listed = (g->n2v_prepared && g->n2v_mode == GW_N2V_REJECTION && g->d.bs_nbr) ? 1 : 0;
   return GW_OK;

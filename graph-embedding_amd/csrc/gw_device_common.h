@@ -34,25 +34,43 @@ __device__ __forceinline__ int64_t gw_row_find(const int32_t* __restrict__ nbrs,
   return (lo < e && nbrs[lo] == key) ? lo : -1;
 }
 
-// Exact neighbour sets for has_edge (GW_N2V_REJECTION): row r owns 2*deg(r)
-// int32 slots at 2*offsets[r] (load factor 1/2, linear probing from a
-// multiply-shift hash); a query reads one slot run, almost always inside one
-// 64 B sector (built by k_build_ehash, gw_n2v.hip).
-__device__ __forceinline__ uint32_t gw_eh_slot(int32_t key, uint32_t cap) {
-  return (uint32_t)(((uint64_t)((uint32_t)key * 0x9E3779B1u) * (uint64_t)cap) >> 32);
+// Exact neighbour sets for has_edge (GW_N2V_REJECTION): row r owns deg(r)
+// buckets of 4 int32 slots (one 16 B-aligned dwordx4) at 4*offsets[r] (load
+// factor 1/4).  A key hashes (multiply-shift) to a bucket and takes its first
+// free slot, else the next bucket's (k_build_ehash, gw_n2v.hip), so a
+// bucket's keys are a prefix of it and a bucket with a free slot ends every
+// query that reaches it: one 16 B read answers a query unless the bucket is
+// full (~1% of queries), never crossing a cache line.  (Round 1-4: 2*deg
+// int32 slots with linear probing — 2.5 dependent slot reads per miss.)
+__device__ __forceinline__ uint32_t gw_eh_slot(int32_t key, uint32_t buckets) {
+  return (uint32_t)(((uint64_t)((uint32_t)key * 0x9E3779B1u) * (uint64_t)buckets) >> 32);
 }
-__device__ __forceinline__ bool gw_eh_has(const int32_t* __restrict__ eh, int64_t rb, int64_t re, int32_t key) {
-  const uint32_t cap = (uint32_t)(2 * (re - rb));
-  if (cap == 0) return false;
-  const int32_t* __restrict__ t = eh + 2 * rb;
-  uint32_t s = gw_eh_slot(key, cap);
-  for (uint32_t i = 0; i < cap; ++i) {
-    const int32_t k = t[s];
-    if (k == key) return true;
-    if (k == -1) return false;
-    s = s + 1 == cap ? 0u : s + 1;
+__device__ __forceinline__ const int4* gw_eh_row(const int32_t* __restrict__ eh, int64_t rb) {
+  return reinterpret_cast<const int4*>(eh + 4 * rb);
+}
+// one bucket: 1 = key present, 0 = absent, -1 = full without it (continue)
+__device__ __forceinline__ int gw_eh_scan(const int4 v, int32_t key) {
+  if (v.x == key || v.y == key || v.z == key || v.w == key) return 1;
+  return v.w == -1 ? 0 : -1;
+}
+// the rest of a query whose bucket hs was full without the key
+__device__ __forceinline__ bool gw_eh_has_from(const int32_t* __restrict__ eh, int64_t rb, uint32_t buckets,
+                                               uint32_t hs, int32_t key) {
+  const int4* t = gw_eh_row(eh, rb);
+  for (uint32_t i = 1; i < buckets; ++i) {
+    hs = hs + 1 == buckets ? 0u : hs + 1;
+    const int r = gw_eh_scan(t[hs], key);
+    if (r >= 0) return r > 0;
   }
   return false;
+}
+__device__ __forceinline__ bool gw_eh_has(const int32_t* __restrict__ eh, int64_t rb, int64_t re, int32_t key) {
+  const uint32_t nb = (uint32_t)(re - rb);
+  if (nb == 0) return false;
+  const uint32_t hs = gw_eh_slot(key, nb);
+  const int r = gw_eh_scan(gw_eh_row(eh, rb)[hs], key);
+  if (r >= 0) return r > 0;
+  return gw_eh_has_from(eh, rb, nb, hs, key);
 }
 
 // Sequential Vose/Walker alias construction exactly as node2vec.py:116-147:

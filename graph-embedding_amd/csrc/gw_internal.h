@@ -33,7 +33,7 @@ constexpr bool kGwDiag = false;
 //   node_J/q int32/f64[nnz] per-node alias tables (weighted or REPLAY)
 //   edge_off int64[nnz+1], edge_J/q per-edge alias tables (REPLAY only)
 //   bitmap   u32[16*nnz/32] has_edge membership pre-filter (BITSET build; REJECTION when eh does not fit)
-//   eh       int32[2*nnz] per-row open-addressing neighbour sets (REJECTION, p/q != 1)
+//   eh       int32[4*nnz] per-row bucketed neighbour sets (REJECTION, p/q != 1): deg(v) 16 B buckets at 4*offsets[v]
 //   bs_*     per-edge common-neighbour bitsets (BITSET mode, sum(deg^2) bits)
 constexpr uint32_t GW_BS_PACK_D = 65536;  // deg(x) below this: kp and c share one word
 struct gw_bs_nbr {  // GW_N2V_BITSET: one 64 B entry (one HBM sector) per adjacency slot (u -> x)
@@ -88,7 +88,7 @@ struct gw_dev_graph {
   int32_t* edge_J = nullptr;
   double* edge_q = nullptr;
   uint32_t* bitmap = nullptr;  // has_edge pre-filter, 16 bits per entry
-  int32_t* eh = nullptr;       // REJECTION mode: exact has_edge hash, 2*deg(v) int32 slots per row at 2*offsets[v]
+  int32_t* eh = nullptr;       // REJECTION mode: exact has_edge hash, deg(v) buckets of 4 int32 slots at 4*offsets[v]
   uint32_t* bs_region = nullptr;  // GW_N2V_BITSET per-edge regions (gw_n2v_bitset.hip)
   gw_bs_nbr* bs_nbr = nullptr;    // [nnz] neighbour + region offset
   gw_ts_ent* sent = nullptr;      // [nnz] REJECTION mode: {x, deg(x), offsets[x]} per slot
@@ -120,6 +120,7 @@ struct gw_topsim_ws {
   int32_t* touched = nullptr;     // [blocks][touch_cap] claimed overflow slots
   int pipe = 0;                   // pipelined kernel (levels of the next source built by wave 0 during
                                   // the walkers): level / spawner scratch doubled per workgroup
+  int diag_pipe = -1;             // -DGW_DIAG builds: the GW_DIAG_TS_PIPE_MAX override the workspace was made for
   int64_t enum_cap = 0;           // enumerated-node pair updates per source (pipelined kernel)
   int32_t* enum_tgt = nullptr;    // [blocks][2][enum_cap]
   double* enum_val = nullptr;     // [blocks][2][enum_cap]
@@ -162,6 +163,7 @@ struct gw_graph {
   double p = 1.0, q = 1.0;
   int64_t edge_alias_entries = 0;
   int64_t bitset_words = 0;
+  double bs_model_s = -1.0;     // gw_bitset_build_model_s of the resident graph (cached; -1: not computed)
   // TopSim state
   gw_topsim_ws ts;
   // naive SimRank workspace (gw_simrank.hip)

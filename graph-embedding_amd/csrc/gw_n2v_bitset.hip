@@ -1221,12 +1221,11 @@ k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t wal
     uint32_t k = 0;
     bool ret = false;  // outlier return to prev (no entry read)
     // pending probe: first slot of px's run in prev's neighbour hash
-    uint32_t hcap = 0, hs = 0;
-    int32_t h0 = -1;
+    uint32_t hs = 0;
+    int4 h0 = make_int4(-1, -1, -1, -1);
     if (pend) {
-      hcap = 2u * pd;
-      hs = gw_eh_slot(px, hcap);
-      h0 = G.eh[2 * (uint64_t)pb + hs];
+      hs = gw_eh_slot(px, pd);
+      h0 = gw_eh_row(G.eh, pb)[hs];
     }
     if (active && !pend) {
       if (len == 1) {  // first order (node2vec.py:28-29)
@@ -1268,19 +1267,9 @@ k_walk_listed(gw_dev_graph G, LsParams P, int L, int64_t walk_begin, int64_t wal
     }
     __builtin_amdgcn_wave_barrier();
     bool acc = ret, take = false;  // take: adopt the entry in E (else the parked one)
-    if (pend) {  // the probe's first slot arrived: finish the run (rarely more than one slot)
-      bool adj = h0 == px;
-      if (!adj && h0 != -1) {
-        for (uint32_t j = 1; j < hcap; ++j) {
-          hs = hs + 1 == hcap ? 0u : hs + 1;
-          const int32_t kk = G.eh[2 * (uint64_t)pb + hs];
-          if (kk == px) {
-            adj = true;
-            break;
-          }
-          if (kk == -1) break;
-        }
-      }
+    if (pend) {  // the probe's bucket arrived: a full bucket (rare) continues the query
+      const int r0 = gw_eh_scan(h0, px);
+      const bool adj = r0 > 0 || (r0 < 0 && gw_eh_has_from(G.eh, pb, pd, hs, px));
       acc = t < (adj ? 1.0 : P.a_q) || trial >= (1u << 24);
       pend = false;
     } else if (sec != 0ull) {
@@ -1610,6 +1599,9 @@ int gw_dev_bitset_build(gw_graph* g, int64_t budget_bytes, bool lists_only) {
 // passes over sum(min(deg u, deg v)) probes plus per-slot header / payload
 // traffic, at rates measured on MI355X; < 0 on a device error.
 double gw_bitset_build_model_s(gw_graph* g) {
+  // GW_N2V_AUTO asks up to three times per prepare (pilot choice, listed_pays
+  // twice): the O(nnz) model kernel runs once per resident graph
+  if (g->bs_model_s >= 0.0) return g->bs_model_s;
   unsigned long long* acc = nullptr;
   if (hipMalloc((void**)&acc, sizeof(unsigned long long)) != hipSuccess) return -1.0;
   unsigned long long w = 0;
@@ -1622,7 +1614,8 @@ double gw_bitset_build_model_s(gw_graph* g) {
   ok = ok && hipMemcpy(&w, acc, sizeof w, hipMemcpyDeviceToHost) == hipSuccess;
   (void)hipFree(acc);
   if (!ok) return -1.0;
-  return 2.0 * (double)w / kBuildProbeRate + (double)g->nnz * kBuildSlotSeconds;
+  g->bs_model_s = 2.0 * (double)w / kBuildProbeRate + (double)g->nnz * kBuildSlotSeconds;
+  return g->bs_model_s;
 }
 
 int gw_dev_walk_bitset_launch(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int64_t walk_count,

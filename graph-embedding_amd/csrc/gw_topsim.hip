@@ -49,7 +49,8 @@ struct TsArgs {
   int variant;
   int diag;  // GW_DIAG_TS (timing experiments only, wrong results): 1 = walkers skip computePathSim, 2 = cheap RNG,
              // 4 / 8 = walker reads confined to the first 2^26 / 2^27 slot entries;
-             // A/B knob (same results): 32 = no deferred ordering
+             // A/B knobs (same results): 32 = no deferred ordering, 512 = new LDS-hash keys reserved on a shared
+             // load counter (round 4), 1024 = a walker's pair update before its next entry load (round 4)
   int sample;
   double sampled;
   double cache[16];
@@ -617,14 +618,42 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       return;
     }
     uint32_t h = H::slot(target);
-    if (kGwDiag && (A.diag & 512)) {  // experiment: no shared load counter, a probe-length cap instead
-      for (int probe = 0; probe < 64; ++probe) {
-        const int32_t k = s_hkey[h];
-        if (k == target || (k == -1 && (atomicCAS(&s_hkey[h], -1, target) == -1 || s_hkey[h] == target))) {
-          atomicAdd(&s_hval[h], val);
-          return;
+    // A new key claims an empty slot with one CAS; a key whose first
+    // kProbeCap slots are taken goes to the HBM overflow hash.  (Round 4
+    // reserved every new key on ONE shared load counter first — P10M sources
+    // insert ~2,700 new keys per ~2,870 updates, so that counter serialised
+    // nearly every update: -2.4% P10M without it; diag bit 512 restores it.)
+    // Slots are never freed while a source accumulates, so a key's chain
+    // never changes: a key is either in its first kProbeCap slots or in the
+    // overflow hash, never both.
+    // The keys are read four at a time (one ds_read_b128 of the aligned
+    // group holding the probe position), so a chain of up to kProbeCap = 16
+    // slots costs at most five LDS reads; at the stretch workload (SAMPLE
+    // 10000: ~36k distinct targets per source) the table fills and every new
+    // key pays the whole cap before it overflows.
+    constexpr int kProbeCap = 16;
+    if (!(kGwDiag && (A.diag & 512))) {
+      int probed = 0;
+      while (probed < kProbeCap) {
+        const uint32_t g0 = h & ~3u;
+        const int4 kv = *reinterpret_cast<const int4*>(&s_hkey[g0]);
+        const int32_t ks[4] = {kv.x, kv.y, kv.z, kv.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if ((uint32_t)j < (h & 3u) || probed >= kProbeCap) continue;
+          ++probed;
+          const uint32_t sl = g0 + (uint32_t)j;
+          int32_t k = ks[j];
+          if (k == -1) {  // claim it; a lost race leaves the winner's key
+            const int32_t old = atomicCAS(&s_hkey[sl], -1, target);
+            k = old == -1 ? target : old;
+          }
+          if (k == target) {
+            atomicAdd(&s_hval[sl], val);
+            return;
+          }
         }
-        h = H::next(h);
+        h = g0 + 4u == (uint32_t)HASH_SLOTS ? 0u : g0 + 4u;
       }
       ov_add(target, val);
       return;
@@ -722,40 +751,50 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     for (int t = 0; t <= L; ++t)
       if (t == l0) dcur = dpath[t];
     bool alive = true;
-    // the draw of step t depends on (s, g, t) only: step t+1's Philox block is
-    // computed while step t's entry load is in flight, off the dependent chain
-    const bool hoist = !(kGwDiag && (A.diag & 128));  // diag bit 128: draw after the load (A/B)
-    gw_u4 un = {0u, 0u, 0u, 0u};
-    if (hoist) un = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)(l0 + 1), 0u, A.k0, A.k1);
+    // The draw of step t depends on (s, g, t) only, so step t+1's Philox block
+    // is computed while step t's entry load is in flight, and step t+1's
+    // entry load is issued BEFORE step t's computePathSim: the LDS-hash probe /
+    // insert of a pair update runs while the next random read is in flight
+    // instead of on the walker's chain of dependent loads.
+    const bool early = !(kGwDiag && (A.diag & 1024));  // diag bit 1024: contrib before the next load (A/B)
+    auto slot_of = [&](const gw_u4& u, int t) -> uint64_t {
+      uint32_t ux = u.x, uy = u.y;
+      if (kGwDiag && (A.diag & 2)) {  // timing only: cheap hash instead of Philox
+        ux = ((uint32_t)s * 0x9E3779B1u) ^ ((uint32_t)g * 0x85EBCA6Bu) ^ ((uint32_t)t * 0xC2B2AE35u);
+        ux ^= ux >> 15;
+        ux *= 0x2C1B3C6Du;
+        uy = 0u;
+      }
+      uint64_t ei = (uint64_t)ocur + gw_index(ux, uy, (uint32_t)dcur);
+      if (kGwDiag && (A.diag & 12))  // timing only: walker reads confined to 1 GB / 2 GB of the table
+        ei &= (A.diag & 4) ? ((1ull << 26) - 1) : ((1ull << 27) - 1);
+      return ei;
+    };
+    gw_u4 un = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)(l0 + 1), 0u, A.k0, A.k1);
+    gw_ts_ent en = {0, 0, 0};  // step t's entry, requested during step t-1
+    bool inflight = false;
 #pragma unroll
     for (int t = 1; t <= L; ++t) {
       if (t > l0 && alive) {
-        if (dcur == 0) {
+        if (!inflight && dcur == 0) {
           alive = false;
         } else {
-          uint32_t ux, uy = 0u;
-          if (kGwDiag && (A.diag & 2)) {
-            ux = ((uint32_t)s * 0x9E3779B1u) ^ ((uint32_t)g * 0x85EBCA6Bu) ^ ((uint32_t)t * 0xC2B2AE35u);
-            ux ^= ux >> 15;
-            ux *= 0x2C1B3C6Du;
-          } else if (hoist) {
-            ux = un.x;
-            uy = un.y;
-          } else {
-            const gw_u4 u = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)t, 0u, A.k0, A.k1);
-            ux = u.x;
-            uy = u.y;
+          if (!inflight) {  // the walker's first step
+            en = gw_ts_load(A.ent + slot_of(un, t));  // randNeighbor
+            if (t < L) un = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)(t + 1), 0u, A.k0, A.k1);
           }
-          uint64_t ei = (uint64_t)ocur + gw_index(ux, uy, (uint32_t)dcur);
-          if (kGwDiag && (A.diag & 12))  // timing only: walker reads confined to 1 GB / 2 GB of the table
-            ei &= (A.diag & 4) ? ((1ull << 26) - 1) : ((1ull << 27) - 1);
-          const gw_ts_ent e = gw_ts_load(A.ent + ei);  // randNeighbor
-          if (hoist && t < L) un = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)(t + 1), 0u, A.k0, A.k1);
+          const gw_ts_ent e = en;
+          inflight = false;
           path[t] = e.x;
           dpath[t] = e.d;
           dcur = e.d;
           ocur = e.off;
           ++my_ext;
+          if (early && t < L && dcur != 0) {  // step t+1's read, then step t's pair update
+            en = gw_ts_load(A.ent + slot_of(un, t + 1));
+            inflight = true;
+            if (t + 1 < L) un = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)(t + 2), 0u, A.k0, A.k1);
+          }
           if ((t & 1) == 0 && !(kGwDiag && (A.diag & 1))) contrib(path, dpath, t / 2, s, mw);
         }
       }
@@ -1256,6 +1295,9 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         // deferred ordering: the selected entries go to the workgroup's HBM
         // scratch; the last wave ranks them during the next walker phase
         for (int k = tid; k < cnt; k += BLOCK) {
+          // k made opaque here: otherwise the per-lane 64-bit store address is
+          // hoisted out of the source loop and spilled (12 B scratch at STEP 5)
+          asm volatile("" : "+v"(k));
           A.dsel_id[blk * TOPK_MAX + k] = s_sel_id[k];
           A.dsel_val[blk * TOPK_MAX + k] = s_sel_val[k];
         }
@@ -1441,6 +1483,13 @@ hipError_t launch(int step, int mode, bool pipe, const TsArgs& A, int blocks, si
 
 }  // namespace
 
+// -DGW_DIAG builds only: GW_DIAG_TS_PIPE_MAX=N runs the pipelined hash-mode
+// kernel up to SAMPLE N instead of kPipeMaxSample (A/B knob; -1: no override)
+static int diag_pipe_max() {
+  const char* v = GW_DIAG_ENV("GW_DIAG_TS_PIPE_MAX");
+  return v ? std::atoi(v) : -1;
+}
+
 int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int topk) {
   if (g->device < 0) {
     g->err = "graph is not on a device (call gw_graph_to_device)";
@@ -1523,10 +1572,12 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   // pipelined at any SAMPLE: its single workgroup otherwise leaves the CU idle
   // of walker reads during every level / output phase (blog, SAMPLE 10000:
   // 10.32 vs 10.52 ms, profiles/r04/ts_knob_ab_defer_order_pipe_row.jsonl).
+  const int64_t pipe_max = diag_pipe_max() >= 0 ? diag_pipe_max() : kPipeMaxSample;
   bool pipe = variant == GW_TOPSIM_SINGLE_SAMPLE &&
-              ((mode == 2 && sample <= kPipeMaxSample) || (mode == 0 && (size_t)n * 8 > TS_2WG_LDS));
+              ((mode == 2 && sample <= pipe_max) || (mode == 0 && (size_t)n * 8 > TS_2WG_LDS));
   if (const char* np = GW_DIAG_ENV("GW_DIAG_TS_NOPIPE"))  // A/B knob: the unpipelined kernel
     if (np[0] == '1') pipe = false;
+  t.diag_pipe = diag_pipe_max();
   const int64_t nb = pipe ? 2 : 1;
   const int64_t enum_cap = pipe ? (int64_t)step * level_cap : 1;
   const int64_t per_block = nb * ((int64_t)(L + 1) * level_cap * 20 + spawn_cap * 20 + 4) + 2 * level_cap * 8 +
@@ -1593,7 +1644,7 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
                   const gw_ts_sparse* sparse) {
   gw_topsim_ws& t = g->ts;
   if (t.blocks == 0 || t.variant != variant || t.sample != sample || t.step != step ||
-      (out_ids_dev && topk > t.topk)) {
+      (out_ids_dev && topk > t.topk) || (kGwDiag && t.diag_pipe != diag_pipe_max())) {
     int rc = gw_dev_topsim_prepare(g, variant, sample, step, std::max(topk, t.topk > 0 ? t.topk : topk));
     if (rc != GW_OK) return rc;
   }

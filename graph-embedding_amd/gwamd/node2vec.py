@@ -21,6 +21,14 @@ uploads the graph: the sampler is prepared by the first `simulate_walks`, once
 num_walks * n * (walk_length - 1) steps are known, with GW_N2V_AUTO by default
 (the per-edge bitset sampler when its build pays back over those steps, else
 the rejection sampler; `sampler="bitset"` / `"rejection"` force one).
+
+Walk bits in scale mode: both samplers draw every walk from the reference's
+law, but with different draws, so for a given `seed` the walk at a given
+index depends on the sampler — and under the default `sampler="auto"` the
+sampler depends on the FIRST `simulate_walks` call's workload (the choice
+then sticks for later calls on the same Graph).  Callers that need walks that
+are bit-stable across different `num_walks` (e.g. a prefix of a larger run)
+pass `sampler="rejection"` or `sampler="bitset"` explicitly.
 """
 import random
 from collections.abc import Mapping

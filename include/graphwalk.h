@@ -71,11 +71,16 @@ extern "C" {
 #define GW_N2V_REPLAY 0
 /* scale mode: per-node alias only (or none when unweighted); second-order
  * bias by exact rejection sampling with the return edge as an outlier;
- * Philox4x32-10 keyed by (seed, walk, step, trial).  On unweighted undirected
- * NX_SIMPLE graphs prepare also builds 64 B listed slot entries (common
- * neighbours of each edge's endpoints when they fit 40 B) that answer most
- * has_edge probes; they take 64 B per adjacency entry and are skipped (same
- * walks, 16 B entries) when they exceed half of the free HBM.              */
+ * Philox4x32-10 keyed by (seed, walk, step, trial).  Unweighted undirected
+ * NX_SIMPLE graphs: prepare builds 16 B slot entries {x, deg x, offsets x}
+ * and per-row neighbour hash sets (16 B buckets); at q > 1 a step whose
+ * deg(prev) < deg(cur) draws from the exact N(cur)/N(prev) mixture proposal,
+ * otherwise from the uniform proposal with a lazy has_edge probe.  64 B
+ * listed entries (common neighbours of each edge when they fit 40 B, which
+ * answer most lazy probes) are built for q < 1 only, whatever
+ * gw_options_t.listed says (at q >= 1 they would answer no probe), and are
+ * skipped (same walks, 16 B entries) when they exceed half of the free HBM.
+ * The walks never depend on which tables were built.                       */
 #define GW_N2V_REJECTION 1
 /* exact second-order sampling from per-edge common-neighbour bitsets (the
  * reference's per-edge alias tables compressed to 1 bit per entry, sum(deg^2)
@@ -128,8 +133,9 @@ typedef struct gw_options_t {
    * listed = -1, GW_N2V_REJECTION builds its 64 B listed entries only when
    * their modelled build time is paid back over these steps; 0 = unknown   */
   int64_t expected_steps;
-  /* GW_N2V_REJECTION listed entries: -1 = by expected_steps (unknown: build
-   * whenever they fit), 0 = never, 1 = whenever they fit                   */
+  /* GW_N2V_REJECTION listed entries, considered for q < 1 only (never built
+   * at q >= 1): -1 = by expected_steps (unknown: build whenever they fit),
+   * 0 = never, 1 = whenever they fit                                       */
   int32_t listed;
   /* gw_simrank_naive input row: 0 = in LDS when it fits, 1 = in HBM (same
    * result bits; exists for tests and very large m)                        */

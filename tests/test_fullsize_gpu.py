@@ -112,40 +112,72 @@ def test_p10m_topsim_sources(gw, oracle):
         assert np.all(np.diff(S[r, :k]) <= 0) and s not in I[r, :k] and np.all(S[r, :k] > 0)
 
 
-def _one_walk_per_vertex(gw, oracle, G, p, q, mode, seed, oracle_fn):
+def _walks_per_vertex(gw, oracle, G, p, q, mode, seed, oracle_fn, R=1):
+    """R walks from every vertex (R iterations of the keyed shuffle) in ONE
+    launch: every iteration's starts a permutation, lengths, counters, sampled
+    steps follow edges, and bit-exact oracle windows at the start, the middle
+    and the end of the launch.  Returns trials per step."""
     import torch
     from gwamd import _lib as C
     C.check(C.lib().gw_n2v_prepare(G.handle, p, q, mode), G.handle)
     n, L = G.n, 80
-    out = torch.empty((n, L), dtype=torch.int32, device="cuda")
-    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    tot = n * R
+    out = torch.empty((tot, L), dtype=torch.int32, device="cuda")
+    lens = torch.empty(tot, dtype=torch.int32, device="cuda")
     cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
-    C.check(C.lib().gw_n2v_walks(G.handle, L, seed, 0, n, 1, C.ptr(out), C.ptr(lens), C.ptr(cnt), None), G.handle)
+    C.check(C.lib().gw_n2v_walks(G.handle, L, seed, 0, tot, 1, C.ptr(out), C.ptr(lens), C.ptr(cnt), None), G.handle)
     torch.cuda.synchronize()
     csr = G.export_csr()
     offs, nbrs = csr["offsets"], csr["nbrs"]
     deg = np.diff(offs)
     starts = out[:, 0].cpu().numpy()
-    np.testing.assert_array_equal(np.sort(starts), np.arange(n))  # iteration 0 starts every vertex once
+    for it in sorted({0, R - 1}):  # every iteration starts every vertex once
+        np.testing.assert_array_equal(np.sort(starts[it * n:(it + 1) * n]), np.arange(n))
     ln = lens.cpu().numpy()
     np.testing.assert_array_equal(ln, np.where(deg[starts] > 0, L, 1))
     assert int(cnt[0].item()) == int((ln - 1).sum())
-    rows = np.random.default_rng(0).integers(0, n, 2000)
+    rows = np.random.default_rng(0).integers(0, tot, 2000)
     W = out[torch.as_tensor(rows, device="cuda")].cpu().numpy()
     W = W[ln[rows] == L]
     assert _is_edge(offs, nbrs, W[:, :-1].ravel(), W[:, 1:].ravel()).all()
-    for begin in (0, n // 2 + 777, n - 1000):
+    for begin in (0, tot // 2 + 777, tot - 1000):
         ref, rl, _ = oracle_fn(csr, p, q, seed, L, begin, 1000, nthreads=8)
         np.testing.assert_array_equal(out[begin:begin + 1000].cpu().numpy(), ref)
         np.testing.assert_array_equal(ln[begin:begin + 1000], rl)
     return int(cnt[1].item()) / max(int(cnt[0].item()), 1)
 
 
+def _one_walk_per_vertex(gw, oracle, G, p, q, mode, seed, oracle_fn):
+    return _walks_per_vertex(gw, oracle, G, p, q, mode, seed, oracle_fn, 1)
+
+
+def _scale_oracle(oracle):
+    return lambda c, *a, **k: oracle.walks_scale(dict(c, weights=None), *a, **k)
+
+
+def test_headline_config_rejection_mixture_walks(gw, oracle):
+    """Config 2 through GW_N2V_REJECTION: the one-shot sampler (q > 1: the
+    exact N(cur)/N(prev) mixture proposal) that GW_N2V_AUTO and the bench's
+    end_to_end_best pick for ONE BASELINE pass (node2vec.py:41-81)."""
+    from gwamd import _lib as C
+    G = gw.GWGraph.rmat(20, 16, 0.57, 0.19, 0.19, 42).to_device(0)
+    G.options(listed=0)
+    trials = _walks_per_vertex(gw, oracle, G, 0.25, 4.0, C.N2V_REJECTION, 42, _scale_oracle(oracle), 10)
+    assert 1.0 <= trials < 3.0  # mixture proposal: ~2 trials per step at R-MAT-20 p=0.25 q=4
+
+
+def test_northstar_rejection_mixture_rmat24_ef6(gw, oracle):
+    from gwamd import _lib as C
+    G = gw.GWGraph.rmat(24, 6, 0.57, 0.19, 0.19, 43).to_device(0)
+    G.options(listed=0)
+    trials = _one_walk_per_vertex(gw, oracle, G, 0.25, 4.0, C.N2V_REJECTION, 42, _scale_oracle(oracle))
+    assert 1.0 <= trials < 3.0
+
+
 def test_config4_rejection_rmat24(gw, oracle):
     from gwamd import _lib as C
     G = gw.GWGraph.rmat(24, 16, 0.57, 0.19, 0.19, 42).to_device(0)
-    fn = lambda c, *a, **k: oracle.walks_scale(dict(c, weights=None), *a, **k)  # noqa: E731
-    trials = _one_walk_per_vertex(gw, oracle, G, 1.0, 0.5, C.N2V_REJECTION, 42, fn)
+    trials = _one_walk_per_vertex(gw, oracle, G, 1.0, 0.5, C.N2V_REJECTION, 42, _scale_oracle(oracle))
     assert 1.0 <= trials < 1.1  # lazy rejection: ~1.03 trials per step at p=1 q=0.5
 
 

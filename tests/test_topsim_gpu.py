@@ -120,6 +120,44 @@ def test_topk_selection(gw, oracle, name, k):
         assert np.all(ids[r, len(got):] == -1) and np.all(sc[r, len(got):] == 0.0)
 
 
+@pytest.mark.parametrize("sample,step,stride", [(1500, 5, 8), (1000, 3, 8)])
+def test_topk_pipelined_many_sources_per_workgroup(gw, oracle, sample, step, stride):
+    """The hash-mode pipelined kernel's deferred ordering (the last wave ranks
+    source r's top-k while the workgroup walks source r+1) runs only when one
+    workgroup handles two or more sources: arxiv at SAMPLE <= 2048 on every
+    8th vertex (4,843 sources, ~5 per workgroup) against oracle.topsim_topk
+    (same walks and sums; ranked score desc / id asc)."""
+    import torch
+    from gwamd import _lib as Cl
+    g = _graph(gw, "arxiv")
+    n, K = g.getVCount(), 20
+    sources = np.arange(0, n, stride, dtype=np.int32)
+    g._ensure_device()
+    src = torch.as_tensor(sources, device="cuda")
+    ids = torch.empty((len(src), K), dtype=torch.int32, device="cuda")
+    sc = torch.empty((len(src), K), dtype=torch.float64, device="cuda")
+    st = torch.zeros(4, dtype=torch.int64, device="cuda")
+    h = g._g.handle
+    Cl.check(Cl.lib().gw_topsim(h, 0, sample, step, 0.6, 11, Cl.ptr(src), len(src), K, Cl.ptr(ids), Cl.ptr(sc),
+                                Cl.ptr(st), None), h)
+    I, S = ids.cpu().numpy(), sc.cpu().numpy()
+    oi, osc, ost = oracle.topsim_topk(g._offs, g._nbrs, 0, sample, step, K, C=0.6, seed=11, sources=sources,
+                                      nthreads=8)
+    stg = st.cpu().numpy()
+    assert int(stg[0]) == ost["extensions"] and int(stg[1]) == ost["pair_updates"]
+    for r in range(len(sources)):
+        m = int((oi[r] >= 0).sum())
+        got = I[r][I[r] >= 0]
+        assert len(got) == m
+        np.testing.assert_allclose(S[r, :m], osc[r, :m], rtol=1e-12)
+        omap = dict(zip(oi[r, :m].tolist(), osc[r, :m].tolist()))
+        for k, (a, b) in enumerate(zip(got.tolist(), oi[r, :m].tolist())):  # ids equal except at fp-noise ties
+            if a != b:
+                sa = omap.get(a, S[r, k])
+                assert abs(sa - osc[r, k]) <= 1e-12 * osc[r, k]
+        assert np.all(I[r, m:] == -1) and np.all(S[r, m:] == 0.0)
+
+
 def test_mirror_compute_and_print(gw, oracle, tmp_path):
     """TopSim_singleSample mirror + printByOrder on GPU dense rows == Java
     emulation over the oracle rows."""

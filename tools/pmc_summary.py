@@ -50,11 +50,18 @@ def mean_counter(rs, counter, kre, grid):
 
 
 def lines(bench):
-    yield bench.get("roofline") or {}
+    """Every roofline dict of a bench line: the headline, each secondary (and
+    its `more` entries) and the one-shot rejection-sampler legs
+    (`end_to_end_rejection.roofline`)."""
+    def of(d):
+        d = d or {}
+        yield d.get("roofline") or {}
+        yield (d.get("end_to_end_rejection") or {}).get("roofline") or {}
+    yield from of(bench)
     for v in (bench.get("secondary") or {}).values():
-        yield (v or {}).get("roofline") or {}
+        yield from of(v)
         for m in (v or {}).get("more", []) or []:
-            yield m.get("roofline") or {}
+            yield from of(m)
 
 
 def main():

@@ -6,7 +6,13 @@ the same box state.  Also reports the counters and the top-k agreement of
 every variant with the first (fp64 atomics make the last bits order-dependent).
 
     python tools/ts_lib_ab.py main abl/ts_flat.so [--graphs p10m,blog,arxiv] [--reps 4]
-("main" = the in-tree gwamd/libgraphwalk.so)
+("main" = the in-tree gwamd/libgraphwalk.so, "diag" = gwamd/libgraphwalk_diag.so;
+"LIB:VAR=value" sets that environment variable around the variant's launches,
+e.g. diag:GW_DIAG_TS=1024 — entries naming the same library share ONE library
+instance and ONE graph handle, so a knob A/B sees the same allocations
+("diag#2:VAR=value" gets a handle of its own);
+--sample / --step / --stride override the P10M workload, e.g. the config-5
+stretch SAMPLE 10000 / STEP 5 on every 16th source)
 
 Two library instances in one process can differ by up to ~5% on P10M by the
 placement of their tables alone (profiles/r04/ts_lib_ab_three_way.jsonl), so
@@ -45,6 +51,10 @@ def main():
     ap.add_argument("--graphs", default="p10m,blog,arxiv")
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--procs", type=int, default=0, help="rounds of one child process per library")
+    ap.add_argument("--sample", type=int, default=1000, help="P10M SAMPLE")
+    ap.add_argument("--step", type=int, default=3, help="P10M STEP")
+    ap.add_argument("--stride", type=int, default=1, help="P10M: every stride-th non-isolated source")
+    ap.add_argument("--ls-sample", type=int, default=0, help="lshrank graphs: SAMPLE (default 10000)")
     a = ap.parse_args()
     if a.procs > 0:
         import subprocess
@@ -68,22 +78,41 @@ def main():
     import numpy as np
     import torch
     from gwamd import _lib as C
-    paths = [os.path.join(ROOT, "graph-embedding_amd", "gwamd", "libgraphwalk.so") if x == "main"
-             else os.path.join(ROOT, x) for x in a.libs]
-    libs = [load(p, C) for p in paths]
+    def path_of(x):
+        x = x.split(":")[0].split("#")[0]
+        if x in ("main", "diag"):
+            return os.path.join(ROOT, "graph-embedding_amd", "gwamd",
+                                "libgraphwalk.so" if x == "main" else "libgraphwalk_diag.so")
+        return os.path.join(ROOT, x)
+    envs = [dict([x.split(":", 1)[1].split("=", 1)]) if ":" in x else {} for x in a.libs]
+    paths = [path_of(x) for x in a.libs]
+    loaded = {}
+    for pth in paths:
+        if pth not in loaded:
+            loaded[pth] = load(pth, C)
+    libs = [loaded[pth] for pth in paths]
+    # entries of one library share its graph handle (a "#tag" after the path
+    # gives an entry its own handle: knobs read when the workspace is sized,
+    # e.g. GW_DIAG_TS_PIPE_MAX, must not re-prepare inside the timed launches)
+    hkey = [x.split(":")[0] for x in a.libs]
+    first_of = [hkey.index(k) for k in hkey]
     dev = torch.device("cuda:0")
     stream = torch.cuda.current_stream(dev)
     sh = ctypes.c_void_p(stream.cuda_stream)
     for gname in a.graphs.split(","):
         hs = []
-        for L in libs:
+        for k, L in enumerate(libs):
+            if first_of[k] != k:
+                hs.append(hs[first_of[k]])
+                continue
             h = ctypes.c_void_p()
             t0 = time.perf_counter()
             if gname == "p10m":
                 rc = L.gw_graph_rmat_java(10_000_000, 100_000_000, 0.57, 0.19, 0.19, 42, ctypes.byref(h))
-                K, sample, step = 100, 1000, 3
+                K, sample, step = 100, a.sample, a.step
             else:
                 f, V, sep, sample, step, K = GRAPHS[gname]
+                sample = a.ls_sample or sample
                 rc = L.gw_graph_load_edgelist(os.path.join(ROOT, "tests", "golden", "data", f).encode(),
                                               sep.encode(), C.SEM_JAVA_MULTI, 0, 0, V, ctypes.byref(h))
             if rc != 0 or L.gw_graph_to_device(h, 0) != 0:
@@ -99,6 +128,8 @@ def main():
         nb = np.empty(max(nnz, 1), np.int32)
         libs[0].gw_graph_export_csr(hs[0], offs.ctypes.data, nb.ctypes.data, None, None, None)
         srcs = np.nonzero(np.diff(offs) > 0)[0].astype(np.int32)
+        if gname == "p10m" and a.stride > 1:
+            srcs = srcs[::a.stride].copy()
         del nb
         src = torch.as_tensor(srcs, device=dev)
         ns = len(srcs)
@@ -110,12 +141,15 @@ def main():
 
         def run(k):
             st.zero_()
+            os.environ.update(envs[k])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             rc = libs[k].gw_topsim(hs[k], C.TOPSIM_SINGLE_SAMPLE, sample, step, 0.6, 42, C.ptr(src), ns, K,
                                    C.ptr(outs[k][0]), C.ptr(outs[k][1]), C.ptr(st), sh)
             e1.record(stream)
             torch.cuda.synchronize()
+            for v in envs[k]:
+                os.environ.pop(v, None)
             if rc != 0:
                 raise SystemExit(libs[k].gw_last_error(hs[k]).decode())
             return e0.elapsed_time(e1)
@@ -136,8 +170,9 @@ def main():
                               "ms": [round(x, 3) for x in times[k]], "vs_first": round(med / base, 4),
                               "stats": stats[k], "ids_equal_frac_vs_first": ids_eq,
                               "max_rel_score_diff_vs_first": rel}), flush=True)
-        for L, h in zip(libs, hs):
-            L.gw_graph_free(h)
+        for k, (L, h) in enumerate(zip(libs, hs)):
+            if first_of[k] == k:
+                L.gw_graph_free(h)
         del outs
         torch.cuda.synchronize()
 
