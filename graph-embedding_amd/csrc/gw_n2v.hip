@@ -569,7 +569,9 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
 //
 // MIX (q > 1): the mixture proposal of k_walk_scale when deg(prev) < deg(cur)
 // (a prev-branch candidate is parked for "x in N(cur)"), the uniform proposal
-// otherwise (parked for "x in N(prev)").
+// otherwise (parked for "x in N(prev)").  !MIX (q < 1; q = 1 never probes):
+// the uniform proposal, whose probes mostly ACCEPT (a candidate passes unless
+// it is a common neighbour), so a parked probe is issued alone.
 template <bool MIX>
 __global__ void __launch_bounds__(kBlock)
 k_walk_rej(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_count, int shuffle,
@@ -622,7 +624,12 @@ k_walk_rej(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_
     bool from_cur = true;   // mixture branch of the candidate
     double t = 0.0;         // uniform proposal: the acceptance draw scaled by M
     double um = 0.0;        // mixture: u.w (acceptance of prev drawn from N(cur))
-    if (active) {
+    // speculate the next trial beside a parked probe only where probes mostly
+    // reject (q > 1: the candidate must be a common neighbour); at q < 1 a
+    // probed candidate is accepted unless it is common, so the speculative
+    // entry would mostly be dropped: the probe goes alone
+    const bool draw = active && (MIX || !park);
+    if (draw) {
       if (len == 1) {  // first order (node2vec.py:28-29)
         const gw_u4 u = gw_philox(c0, c1, 1u, 0u, P.k0, P.k1);
         slot = b + (int64_t)gw_index(u.x, u.z, (uint32_t)d);
@@ -655,7 +662,7 @@ k_walk_rej(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_
       bool acc = false;
       int32_t next = prev;     // the outlier's target
       int64_t nb = pb, nd = pe - pb;  // row of next
-      bool drawn = true;       // this iteration's draw is evaluated (not dropped)
+      bool drawn = draw;       // this iteration's draw is evaluated (not dropped)
       if (park) {
         const int r0 = gw_eh_scan(hv, px);
         const bool adj = r0 > 0 || (r0 < 0 && gw_eh_has_from(G.eh, hrb, hnb, hs, px));

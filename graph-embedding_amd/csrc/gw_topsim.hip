@@ -50,7 +50,8 @@ struct TsArgs {
   int diag;  // GW_DIAG_TS (timing experiments only, wrong results): 1 = walkers skip computePathSim, 2 = cheap RNG,
              // 4 / 8 = walker reads confined to the first 2^26 / 2^27 slot entries;
              // A/B knobs (same results): 32 = no deferred ordering, 512 = new LDS-hash keys reserved on a shared
-             // load counter (round 4), 1024 = a walker's pair update before its next entry load (round 4)
+             // load counter (round 4), 1024 = a walker's pair update before its next entry load (round 4),
+             // 2048 = a walker's last pair update not carried into the lane's next walker
   int sample;
   double sampled;
   double cache[16];
@@ -680,21 +681,28 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
 
   // computePathSim for the path node at depth 2i with mass `mass`
   // (degrees travel with the path: dpath[t] = deg(path[t]))
-  auto contrib = [&](const int32_t* path, const int32_t* dpath, int i, int32_t source, double mass) {
-    const int32_t target = path[2 * i];
-    if (target == source) return;  // TopSim_singleSample.java:183
+  // the pair update of a path node at depth 2i: false when computePathSim
+  // skips it (target == source, or not a first meeting)
+  auto contrib_val = [&](const int32_t* path, const int32_t* dpath, int i, int32_t source, double mass,
+                         int32_t* target, double* val) -> bool {
+    *target = path[2 * i];
+    if (*target == source) return false;  // TopSim_singleSample.java:183
 #pragma unroll
     for (int j = 0; j < STEP; ++j)  // isFirstMeet (:211-218)
-      if (j < i && path[j] == path[2 * i - j]) return;
+      if (j < i && path[j] == path[2 * i - j]) return false;
     const double dm = (double)dpath[i];
     const double dt = (double)dpath[2 * i];
-    double val;
     if (rw)  // SingleRandomWalk.java:89: cache[i]*deg/deg/SAMPLE
-      val = ((A.cache[i] * dm) / dt) / A.sampled;
+      *val = ((A.cache[i] * dm) / dt) / A.sampled;
     else     // TopSim_singleSample.java:189
-      val = ((mass * A.cache[i]) * dm) / dt;
-    add(target, val);
+      *val = ((mass * A.cache[i]) * dm) / dt;
     ++my_upd;
+    return true;
+  };
+  auto contrib = [&](const int32_t* path, const int32_t* dpath, int i, int32_t source, double mass) {
+    int32_t target;
+    double val;
+    if (contrib_val(path, dpath, i, source, mass, &target, &val)) add(target, val);
   };
 
   // PIPE: wave 0 claims the next source and builds its levels into buffer b
@@ -724,7 +732,10 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   };
   // one walker (index g in the reference's BFS queue order) of source s from
   // the level / spawner records of buffer b
-  auto run_walker = [&](int g, int b, int32_t s, int ds, int ns) {
+  // (pt, pv): a pair update carried from the lane's previous walker — the one
+  // of its last step (2*STEP), added after this walker's first entry load is
+  // issued, so it too leaves the chain of dependent loads (pt < 0: none)
+  auto run_walker = [&](int g, int b, int32_t s, int ds, int ns, int32_t& pt, double& pv) {
     const int32_t* Vb = V + b * lvl_stride;
     const int32_t* Db = D + b * lvl_stride;
     const int32_t* Pb = P + b * lvl_stride;
@@ -782,6 +793,10 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           if (!inflight) {  // the walker's first step
             en = gw_ts_load(A.ent + slot_of(un, t));  // randNeighbor
             if (t < L) un = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)(t + 1), 0u, A.k0, A.k1);
+            if (pt >= 0) {  // the previous walker's last pair update
+              add(pt, pv);
+              pt = -1;
+            }
           }
           const gw_ts_ent e = en;
           inflight = false;
@@ -795,7 +810,14 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
             inflight = true;
             if (t + 1 < L) un = gw_philox((uint32_t)s, (uint32_t)g, (uint32_t)(t + 2), 0u, A.k0, A.k1);
           }
-          if ((t & 1) == 0 && !(kGwDiag && (A.diag & 1))) contrib(path, dpath, t / 2, s, mw);
+          if ((t & 1) == 0 && !(kGwDiag && (A.diag & 1))) {
+            if (PIPE && t == L && early && !(kGwDiag && (A.diag & 2048))) {  // carried to the next walker
+              if (pt >= 0) add(pt, pv);  // (not flushed: this walker issued no first load)
+              if (!contrib_val(path, dpath, t / 2, s, mw, &pt, &pv)) pt = -1;
+            } else {
+              contrib(path, dpath, t / 2, s, mw);
+            }
+          }
         }
       }
     }
@@ -1006,6 +1028,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       const int lane = tid & 63;
       const int32_t* ETb = A.enum_tgt + (blk * 2 + cur) * A.enum_cap;
       const double* EVb = A.enum_val + (blk * 2 + cur) * A.enum_cap;
+      int32_t pt = -1;
+      double pv = 0.0;
       for (;;) {
         unsigned base = 0u;
         if (lane == 0) base = atomicAdd(&s_wnext, 64u);
@@ -1013,14 +1037,18 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         if ((int)base >= p_nw + p_ne) break;
         const int g = (int)base + lane;
         if (g < p_nw)
-          run_walker(g, cur, s, ds, p_ns);
+          run_walker(g, cur, s, ds, p_ns, pt, pv);
         else if (g < p_nw + p_ne)
           add(ETb[g - p_nw], EVb[g - p_nw]);
       }
+      if (pt >= 0) add(pt, pv);
     } else {
       const int W = s_nwalk;
       const int ns = s_nspawn;
-      for (int g = tid; g < W; g += BLOCK) run_walker(g, 0, s, ds, ns);
+      int32_t pt = -1;
+      double pv = 0.0;
+      for (int g = tid; g < W; g += BLOCK) run_walker(g, 0, s, ds, ns, pt, pv);
+      if (pt >= 0) add(pt, pv);
     }
     __syncthreads();
 
@@ -1483,6 +1511,50 @@ hipError_t launch(int step, int mode, bool pipe, const TsArgs& A, int blocks, si
 
 }  // namespace
 
+// Does the pipelined hash-mode kernel pay above kPipeMaxSample?  Its wave 0
+// alone builds the next source's enumerated levels while seven waves walk the
+// current one, so it pays while the enumerated part is small next to the
+// walkers.  That part is deterministic (TopSim_singleSample.java:99-116: a
+// path whose mass reaches its degree enumerates every neighbour with
+// mass/degree), so the host replays it for 64 strided non-isolated sources:
+// E = enumerated path extensions, W = walker steps (ceil(mass) walkers of a
+// node with mass < degree at level l take 2*STEP - l steps).  W/E: P10M 35
+// (SAMPLE 1000, STEP 3; the pipeline -7.1%) and 53 (SAMPLE 10000, STEP 5),
+// lshrank arxiv 5.5-8 (levels of thousands of nodes per source at SAMPLE >=
+// 2500), blog 41-85.
+static bool pipe_pays_large_sample(const gw_graph* g, int sample, int step) {
+  const int64_t n = g->n;
+  if (n <= 0 || (int64_t)g->offsets.size() != n + 1) return false;
+  const int L = 2 * step;
+  std::vector<int32_t> src;
+  for (int64_t v = 0; v < n; ++v)
+    if (g->offsets[v + 1] > g->offsets[v]) src.push_back((int32_t)v);
+  if (src.empty()) return false;
+  double E = 0.0, W = 0.0;
+  const int ns = (int)std::min<size_t>(64, src.size());
+  std::vector<std::pair<int32_t, double>> lvl, nxt;
+  for (int k = 0; k < ns; ++k) {
+    lvl.assign(1, {src[(size_t)k * (src.size() - 1) / std::max(ns - 1, 1)], (double)sample});
+    for (int l = 0; l < L && !lvl.empty(); ++l) {
+      nxt.clear();
+      for (const auto& vm : lvl) {
+        const int64_t b = g->offsets[vm.first], e = g->offsets[vm.first + 1];
+        const int64_t d = e - b;
+        if (d == 0) continue;
+        if (vm.second >= (double)d) {
+          for (int64_t j = b; j < e; ++j) nxt.push_back({g->nbrs[j], vm.second / (double)d});
+        } else {
+          W += std::ceil(vm.second) * (double)(L - l);
+        }
+        if (nxt.size() > ((size_t)1 << 22)) return false;  // huge enumerated levels: keep the workgroup build
+      }
+      E += (double)nxt.size();
+      lvl.swap(nxt);
+    }
+  }
+  return W >= 16.0 * std::max(E, 1.0);
+}
+
 // -DGW_DIAG builds only: GW_DIAG_TS_PIPE_MAX=N runs the pipelined hash-mode
 // kernel up to SAMPLE N instead of kPipeMaxSample (A/B knob; -1: no override)
 static int diag_pipe_max() {
@@ -1574,7 +1646,9 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   // 10.32 vs 10.52 ms, profiles/r04/ts_knob_ab_defer_order_pipe_row.jsonl).
   const int64_t pipe_max = diag_pipe_max() >= 0 ? diag_pipe_max() : kPipeMaxSample;
   bool pipe = variant == GW_TOPSIM_SINGLE_SAMPLE &&
-              ((mode == 2 && sample <= pipe_max) || (mode == 0 && (size_t)n * 8 > TS_2WG_LDS));
+              ((mode == 2 && (sample <= pipe_max ||
+                              (diag_pipe_max() < 0 && pipe_pays_large_sample(g, sample, step)))) ||
+               (mode == 0 && (size_t)n * 8 > TS_2WG_LDS));
   if (const char* np = GW_DIAG_ENV("GW_DIAG_TS_NOPIPE"))  // A/B knob: the unpipelined kernel
     if (np[0] == '1') pipe = false;
   t.diag_pipe = diag_pipe_max();
