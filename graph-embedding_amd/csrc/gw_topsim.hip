@@ -1076,19 +1076,26 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       }
       __syncthreads();
     }
-    // hash mode: move the occupied LDS slots to the front once, so the
-    // selection passes below scan only them (the others are left empty)
+    // hash mode: every thread takes its HASH_SLOTS / BLOCK slots into
+    // registers and clears them.  Top-k rows only (no dense / sparse rows,
+    // `regsel`): the selection passes below read those registers — no
+    // compaction, no LDS re-reads, no re-zeroing pass (round 5).  Otherwise the
+    // occupied slots are moved to the front once, so the passes scan only them.
     int NL = 0;
+    constexpr int SPT = LDS_ROW ? 1 : HASH_SLOTS / BLOCK;
+    static_assert(LDS_ROW || HASH_SLOTS % BLOCK == 0, "hash slots per thread");
+    double vv[SPT];  // the values of this thread's slots (an empty slot holds 0.0)
+    const bool regsel = !LDS_ROW && A.out_ids && !A.out_rows && !A.sp.cursor && !(kGwDiag && (A.diag & 4096));
     if (!LDS_ROW) {
-      constexpr int SPT = HASH_SLOTS / BLOCK;
-      static_assert(HASH_SLOTS % BLOCK == 0, "hash slots per thread");
+#pragma unroll
+      for (int i = 0; i < SPT; ++i) vv[i] = s_hval[tid + i * BLOCK];
+    }
+    if (!LDS_ROW && !regsel) {
       int32_t kk[SPT];
-      double vv[SPT];
       int mine = 0;
 #pragma unroll
       for (int i = 0; i < SPT; ++i) {
         kk[i] = s_hkey[tid + i * BLOCK];
-        vv[i] = s_hval[tid + i * BLOCK];
         mine += kk[i] != -1;
       }
       // offsets: an inclusive scan inside the wave and one LDS atomic per
@@ -1121,7 +1128,16 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       __syncthreads();
       NL = s_ncomp;
     }
-    const int NC = LDS_ROW ? n : NL + nov;
+    const int NC = LDS_ROW ? n : NL + nov;  // LDS-side candidates (regsel: the overflow entries only)
+    // the register-held candidates of this thread (regsel; the keys stay in
+    // LDS until the re-zeroing, values in registers: every key's value > 0)
+    auto each_reg = [&](auto&& f) {
+      if (!LDS_ROW && regsel) {
+#pragma unroll
+        for (int i = 0; i < SPT; ++i)
+          if (vv[i] > 0.0) f(i, vv[i]);
+      }
+    };
     auto cand = [&](int idx, int32_t* id, double* val) -> bool {
       if (LDS_ROW) {
         *id = idx;
@@ -1215,6 +1231,10 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           unsigned* const Hn = (pass & 1) ? s_hist : s_hist2;
           const unsigned long long pre = s_prefix, msk = s_mask;
           for (int b = tid; b < 256; b += BLOCK) Hn[b] = 0;
+          each_reg([&](int, double v) {
+            const unsigned long long k = dkey(v);
+            if ((k & msk) == pre) atomicAdd(&H[(k >> shift) & 255], 1u);
+          });
           for (int idx = tid; idx < NC; idx += BLOCK) {
             int32_t id;
             double v;
@@ -1253,6 +1273,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       if (!take_all && !bin_exact) {
         // ties at the threshold: smallest ids first
         long long eq_local = 0;
+        each_reg([&](int, double v) { eq_local += dkey(v) == T; });
         for (int idx = tid; idx < NC; idx += BLOCK) {
           int32_t id;
           double v;
@@ -1269,6 +1290,11 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
             for (int b = tid; b < 256; b += BLOCK) s_hist[b] = 0;
             __syncthreads();
             const unsigned long long pre = s_prefix, msk = s_mask;
+            each_reg([&](int i, double v) {
+              if (dkey(v) != T) return;
+              const unsigned long long k = (unsigned)s_hkey[tid + i * BLOCK];
+              if ((k & msk) == pre) atomicAdd(&s_hist[(k >> shift) & 255], 1u);
+            });
             for (int idx = tid; idx < NC; idx += BLOCK) {
               int32_t id;
               double v;
@@ -1294,15 +1320,37 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       __syncthreads();
       // one LDS atomic per wave and round (ballot + v_mbcnt ranks), not one
       // per selected entry on the same counter
+      auto selected = [&](int32_t id, double v) {
+        const unsigned long long k = dkey(v);
+        return take_all || (bin_exact ? (k & Tmask) >= T : (k > T || (k == T && id <= idT)));
+      };
+      auto append = [&](bool sel, int32_t id, double v) {
+        const unsigned long long sm = __ballot(sel);
+        if (sm) {
+          int wb = 0;
+          if ((tid & 63) == __ffsll(sm) - 1) wb = atomicAdd(&s_cnt, __popcll(sm));
+          wb = __shfl(wb, __ffsll(sm) - 1, 64);
+          const int slot = wb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+          if (sel && slot < TOPK_MAX) {
+            s_sel_id[slot] = id;
+            s_sel_val[slot] = v;
+          }
+        }
+      };
+      if (!LDS_ROW && regsel) {
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+          const int32_t id = vv[i] > 0.0 ? s_hkey[tid + i * BLOCK] : 0;
+          append(vv[i] > 0.0 && selected(id, vv[i]), id, vv[i]);
+        }
+      }
       for (int base = 0; base < NC; base += BLOCK) {
         const int idx = base + tid;
         int32_t id = 0;
         double v = 0.0;
         bool sel = false;
-        if (idx < NC && cand(idx, &id, &v)) {
-          const unsigned long long k = dkey(v);
-          sel = take_all || (bin_exact ? (k & Tmask) >= T : (k > T || (k == T && id <= idT)));
-        }
+        if (idx < NC && cand(idx, &id, &v)) sel = selected(id, v);
         const unsigned long long sm = __ballot(sel);
         if (sm) {
           int wb = 0;
@@ -1376,6 +1424,14 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       for (int j = tid; j < NL; j += BLOCK) {  // occupied slots were compacted to [0, NL)
         s_hval[j] = 0.0;
         s_hkey[j] = -1;
+      }
+      if (regsel) {  // this thread's own occupied slots
+#pragma unroll
+        for (int i = 0; i < SPT; ++i)
+          if (vv[i] > 0.0) {
+            s_hval[tid + i * BLOCK] = 0.0;
+            s_hkey[tid + i * BLOCK] = -1;
+          }
       }
       for (int k = tid; k < nov; k += BLOCK) {
         const int32_t slot = touched[k];

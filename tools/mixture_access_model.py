@@ -15,8 +15,7 @@ computed in closed form from (deg prev, deg cur, common neighbours):
            of prev's neighbour hash (x in N(prev))
 
 and split by branch, by the degree of the probed row, and by the size of the
-probed hash row (2 deg int32 slots: rows of <= 16 neighbours are one 128 B
-line, so the step's later probes of it can hit the cache).
+probed hash row.  At q < 1 (config 4) every step takes the uniform proposal.
 
     python tools/mixture_access_model.py [scale] [p] [q] [edge_factor] [walks]
 """
@@ -59,6 +58,8 @@ def N(v):
 
 
 a_p, a_q = 1 / p, 1 / q
+# q < 1 (config 4): the uniform proposal with the lazy probe at every step;
+# k_walk_rej issues a parked probe alone there (no speculative entry)
 mo = max(0.0, a_p - a_q)
 mprev = min(1.0, a_p / a_q)
 M = max(1.0, a_q)
@@ -84,7 +85,7 @@ for w in range(W.shape[0]):
         Np, Nc = N(prev), N(cur)
         c = len(Nc & Np) - (1 if prev in Np else 0)  # x in N(cur), x != prev, x in N(prev)
         acc['steps'] += 1
-        if dp < dc:
+        if q > 1.0 and dp < dc:  # the mixture proposal exists only at q > 1
             H = mo + dc * a_q + (1 - a_q) * dp
             Z = mo + (dc - 1 + mprev) * a_q + (1 - a_q) * c
             T = H / Z
@@ -97,9 +98,9 @@ for w in range(W.shape[0]):
             pr, pv = tp, cur
         else:
             A = M * dc + ext
-            Z = ext + (1 if True else 0) * min(a_p, M) + (dc - 1) * lo + c * (1 - lo)  # accepted mass
-            # accepted mass, in units of the envelope: outlier ext, prev min(1/p, M), others lo + (1-lo)*adj
-            Z = ext + min(a_p, M) + (dc - 1) * lo + c * (1 - lo)
+            # accepted mass (a candidate's proposal mass is M): the outlier ext,
+            # prev min(1/p, M), a common neighbour 1, any other 1/q
+            Z = ext + min(a_p, M) + c + (dc - 1 - c) * a_q
             T = A / Z
             te = M * dc / Z
             pr = M * (dc - 1) * (1 - lo / M) / Z
