@@ -586,7 +586,8 @@ k_walk_rej(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_
   const int64_t w = walk_begin + (valid ? i : 0);
   const uint32_t c0 = (uint32_t)w, c1 = (uint32_t)((uint64_t)w >> 32);
   int32_t cur = -1, prev = -1;
-  int64_t b = 0, e = 0, pb = 0, pe = 0;  // rows of cur and prev
+  int64_t b = 0, pb = 0;  // rows of cur and prev: (first slot, degree)
+  int32_t dc = 0, dpv = 0;
   int len = L;
   uint32_t trial = 0;  // trials drawn in this step (a parked candidate's included)
   // parked candidate: 0 none, 1 probe x in N(prev), 2 probe x in N(cur)
@@ -600,24 +601,24 @@ k_walk_rej(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_
     cur = G.order[sp];
     len = 1;
     b = G.offsets[cur];
-    e = G.offsets[cur + 1];
+    dc = (int32_t)(G.offsets[cur + 1] - b);
   }
   stage[0] = cur;
   const bool vec_ok = (L & 3) == 0;
   for (;;) {
-    const bool active = len < L && e != b;
+    const bool active = len < L && dc != 0;
     if (__ballot(active) == 0ull) break;
     bool ready = false;
     int flen = 0;
     // ---- this iteration's reads, issued together: the parked candidate's
     // bucket and the entry of the (possibly speculative) next trial
-    const int64_t d = e - b;
+    const int64_t d = dc;
     uint32_t hs = 0u;
     int64_t hrb = 0;
     uint32_t hnb = 0u;
     if (active && park) {
       hrb = park == 1u ? pb : b;
-      hnb = (uint32_t)(park == 1u ? pe - pb : d);
+      hnb = (uint32_t)(park == 1u ? dpv : dc);
       hs = gw_eh_slot(px, hnb);
     }
     int64_t slot = -1;      // candidate slot (-1: return-edge outlier, no read)
@@ -635,8 +636,8 @@ k_walk_rej(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_
         slot = b + (int64_t)gw_index(u.x, u.z, (uint32_t)d);
       } else {
         const gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
-        if (MIX && pe - pb < d) {
-          const int64_t dp = pe - pb;
+        if (MIX && dpv < dc) {
+          const int64_t dp = dpv;
           const double Ac = (double)d * P.a_q;
           const double H = P.mix_o + Ac + (double)dp * P.mix_p;
           const double r = gw_u01(u.z) * H;
@@ -661,7 +662,8 @@ k_walk_rej(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_
     if (active) {
       bool acc = false;
       int32_t next = prev;     // the outlier's target
-      int64_t nb = pb, nd = pe - pb;  // row of next
+      int64_t nb = pb;
+      int32_t nd = dpv;  // row of next
       bool drawn = draw;       // this iteration's draw is evaluated (not dropped)
       if (park) {
         const int r0 = gw_eh_scan(hv, px);
@@ -687,7 +689,7 @@ k_walk_rej(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_
         bool needs = false;  // decided by a probe next iteration
         if (len == 1) {
           acc = true;
-        } else if (MIX && pe - pb < d) {
+        } else if (MIX && dpv < dc) {
           if (slot < 0) {
             acc = true;  // return-edge outlier
           } else if (from_cur) {
@@ -716,7 +718,7 @@ k_walk_rej(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_
         if (park) {
           px = next;
           pnb = nb;
-          pnd = (int32_t)nd;
+          pnd = nd;
         }
       }
       if (acc) {
@@ -724,10 +726,10 @@ k_walk_rej(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_
         trial = 0;
         prev = cur;
         pb = b;
-        pe = e;
+        dpv = dc;
         cur = next;
         b = nb;  // from the slot entry, or prev's row after an outlier return
-        e = nb + nd;
+        dc = nd;
         stage[64 * (len & (kStage - 1))] = cur;
         ready = (len & (kStage - 1)) == kStage - 1;
         flen = len;
