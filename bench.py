@@ -103,6 +103,8 @@ def parse(argv):
     ap.add_argument("--no-p10m", action="store_true", help="skip config 5 as a secondary")
     ap.add_argument("--no-p10m-stretch", action="store_true",
                     help="skip config 5's stretch (SAMPLE 10000, STEP 5) as a secondary")
+    ap.add_argument("--stretch-stride", type=int, default=16,
+                    help="the stretch runs every stride-th P10M source (1 = all 4.8M)")
     ap.add_argument("--no-arxiv", action="store_true",
                     help="skip the arxiv line (same graph as the reference CPU fixture)")
     ap.add_argument("--secondary", choices=["auto", "all", "none"], default="auto",
@@ -926,7 +928,7 @@ def p10m_graph(R, args):
     return _P10M_GRAPH[key]
 
 
-def run_topsim(R, args, name, sample=None, step=None):
+def run_topsim(R, args, name, sample=None, step=None, stride=1):
     """TopSim_singleSample: lshrank graphs (config 3; every rank all sources) or
     P10M (config 5 at SAMPLE 1000 / STEP 3, or the SURVEY §8d stretch
     SAMPLE 10000 / STEP 5; sources split over ranks, strong scaling)."""
@@ -965,9 +967,11 @@ def run_topsim(R, args, name, sample=None, step=None):
         # round-robin split: R-MAT puts the hubs (the expensive sources) at low
         # ids, so contiguous ranges would load rank 0 with most of the work;
         # rows are keyed by source, so any split gives the same rows
+        if stride > 1:  # every stride-th source (the stretch is ~18x config 5's work per source)
+            srcs_all = srcs_all[::stride].copy()
         srcs = srcs_all[rank::world]
         desc = (f"{args.p10m_vertices} vertices, {10 * args.p10m_vertices} R-MAT lines, {len(srcs_all)} non-isolated "
-                f"sources split round-robin over {world} rank(s)")
+                f"sources" + (f" (every {stride}th)" if stride > 1 else "") + f" split round-robin over {world} rank(s)")
         K, sample, step = 100, sample or 1000, step or 3
         scaling = "strong"
         keep = pg
@@ -1027,7 +1031,7 @@ def run_topsim(R, args, name, sample=None, step=None):
                       value=upd / gboth["seconds"], unit="pair-updates/s (top-k rows all-gathered to every rank)",
                       check_blocks_match_sender_checksums=gonly["check_blocks_match_sender_checksums"] and
                       gboth["check_blocks_match_sender_checksums"])
-    tag = f"topsim_{name}_s{sample}_t{step}_k{K}"
+    tag = f"topsim_{name}_s{sample}_t{step}_k{K}" + (f"_stride{stride}" if stride > 1 else "")
     cpu_ts = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu_ts = cpu_baseline_topsim(offs, nbrs, len(offs) - 1, sample, step, args.seed,
@@ -1228,7 +1232,7 @@ def main(argv):
         if not args.no_p10m:
             secondary["topsim_p10m"] = run_topsim(R, args, "p10m")
         if not args.no_p10m_stretch:
-            secondary["topsim_p10m_stretch"] = run_topsim(R, args, "p10m", 10000, 5)
+            secondary["topsim_p10m_stretch"] = run_topsim(R, args, "p10m", 10000, 5, args.stretch_stride)
     if R.rank == 0:
         ngpu = R.ngpu
         res = {

@@ -822,6 +822,7 @@ void gw_dev_release(gw_graph* g) {
   dev_free(t.spawn_level);
   dev_free(t.spawn_first);
   dev_free(t.acc_row);
+  dev_free(t.ov_list);
   dev_free(t.ov_keys);
   dev_free(t.touched);
   dev_free(t.enum_tgt);
@@ -1302,12 +1303,13 @@ int gw_dev_n2v_walks(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int6
   } else if (wt) {
     if (di) GW_LAUNCH(false, true, true);
     else GW_LAUNCH(false, true, false);
-  } else if (!di && g->d.sent && g->d.eh && !(kGwDiag && GW_DIAG_ENV("GW_DIAG_REJ_SCALE"))) {
-    // one round trip per iteration (k_walk_rej); GW_DIAG_REJ_SCALE: k_walk_scale (A/B, same walks)
-    if (P.a_q < 1.0)
-      k_walk_rej<true><<<grid, kBlock, 0, s>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev, len_dev, C);
-    else
-      k_walk_rej<false><<<grid, kBlock, 0, s>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev, len_dev, C);
+  } else if (!di && g->d.sent && g->d.eh && P.a_q > 1.0 && !(kGwDiag && GW_DIAG_ENV("GW_DIAG_REJ_SCALE"))) {
+    // q < 1: a parked probe per iteration (k_walk_rej); GW_DIAG_REJ_SCALE: k_walk_scale (A/B, same walks)
+    k_walk_rej<false><<<grid, kBlock, 0, s>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev, len_dev, C);
+  } else if (kGwDiag && !di && g->d.sent && g->d.eh && P.a_q < 1.0 && GW_DIAG_ENV("GW_DIAG_REJ_PIPE")) {
+    // q > 1: k_walk_scale's mixture kernel is the shipped one (round 5: with the bucketed neighbour hash it runs
+    // at the calibrated request rate, and the parked probe + speculative trial only adds requests); A/B only
+    k_walk_rej<true><<<grid, kBlock, 0, s>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev, len_dev, C);
   } else {
     if (di) GW_LAUNCH(false, false, true);
     else if (P.a_q < 1.0) GW_LAUNCH_MIX(false, false, false, true);  // q > 1: mixture proposal

@@ -42,7 +42,8 @@ constexpr int TS_WAVES = TS_BLOCK / 64;
 constexpr int TOPK_MAX = 256;
 constexpr int TS_CO_LDS = 1792;  // child / spawner offsets kept in LDS up to this many entries
 constexpr int64_t LDS_ROW_MAX_BYTES = 96 * 1024;
-constexpr int kPipeMaxSample = 2048;  // k_topsim_pipe for SAMPLE up to this
+constexpr int kPipeMaxSample = 2048;  // k_topsim_pipe for SAMPLE up to this (above: pipe_pays_large_sample)
+constexpr int kTsProbeCap = 16;       // LDS-hash slots a key may probe before it overflows to HBM
 
 struct TsArgs {
   gw_dev_graph G;
@@ -78,6 +79,7 @@ struct TsArgs {
   double* spawn_mass;
   int32_t* ov_keys;
   double* ov_vals;
+  double* ov_list;  // [blocks][touch_cap] the compacted overflow values of a source (keys in `touched`)
   int32_t* enum_tgt;  // pipelined kernel: enumerated-node pair updates of a source, [blocks][2][enum_cap]
   double* enum_val;
   int64_t enum_cap;
@@ -562,6 +564,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   int32_t* s_hkey = reinterpret_cast<int32_t*>(s_row + HASH_SLOTS);  // [HASH_SLOTS]
   int32_t* ov_key = LDS_ROW ? nullptr : (A.ov_keys + blk * A.touch_cap);
   double* ov_val = LDS_ROW ? nullptr : (A.ov_vals + blk * A.touch_cap);
+  double* ov_list = LDS_ROW ? nullptr : (A.ov_list + blk * A.touch_cap);
   int32_t* touched = LDS_ROW ? nullptr : (A.touched + blk * A.touch_cap);
   const uint32_t ov_mask = (uint32_t)(A.touch_cap - 1);
   const bool rw = !PIPE && (A.variant == GW_TOPSIM_SINGLE_RW);  // PIPE: TopSim_singleSample only
@@ -619,21 +622,29 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       return;
     }
     uint32_t h = H::slot(target);
-    // A new key claims an empty slot with one CAS; a key whose first
-    // kProbeCap slots are taken goes to the HBM overflow hash.  (Round 4
-    // reserved every new key on ONE shared load counter first — P10M sources
-    // insert ~2,700 new keys per ~2,870 updates, so that counter serialised
-    // nearly every update: -2.4% P10M without it; diag bit 512 restores it.)
-    // Slots are never freed while a source accumulates, so a key's chain
-    // never changes: a key is either in its first kProbeCap slots or in the
-    // overflow hash, never both.
+    // A new key claims an empty slot with one CAS, once a plain read of the
+    // workgroup's load counter says the table is below HASH_LIMIT (75%), and
+    // then bumps the counter with a non-returning LDS add; a key whose first
+    // kTsProbeCap slots are taken, or that finds the table at its limit, goes
+    // to the HBM overflow hash.  (Round 4 reserved every new key with a
+    // RETURNING add on the shared counter first — P10M sources insert ~2,700
+    // new keys per ~2,870 updates, so the counter serialised nearly every
+    // update; diag bit 512 restores it.  With no limit at all, diag bit 8192,
+    // a table that fills up — arxiv at SAMPLE 10000, the P10M stretch — makes
+    // every new key walk the whole cap.)  Slots are never freed while a
+    // source accumulates, so a key's chain never changes: a key is in its
+    // first kTsProbeCap slots or in the overflow hash; the rare key that a
+    // racing counter read lets into both is folded before selection.
     // The keys are read four at a time (one ds_read_b128 of the aligned
-    // group holding the probe position), so a chain of up to kProbeCap = 16
-    // slots costs at most five LDS reads; at the stretch workload (SAMPLE
-    // 10000: ~36k distinct targets per source) the table fills and every new
-    // key pays the whole cap before it overflows.
-    constexpr int kProbeCap = 16;
+    // group holding the probe position): a chain of up to 16 slots costs at
+    // most five LDS reads.
     if (!(kGwDiag && (A.diag & 512))) {
+      // the table at its load limit (read once per update): no more claims.
+      // (pipelined STEP >= 5 kernels go without the limit: at 125 of 128 VGPRs the
+      // extra live state spills 40 B in k_topsim_pipe<5>.)
+      constexpr bool kLimit = STEP < 5 || !PIPE;
+      const bool full = kLimit && !(kGwDiag && (A.diag & 8192)) && *(volatile int*)&s_hcount >= HASH_LIMIT;
+      constexpr int kProbeCap = kTsProbeCap;
       int probed = 0;
       while (probed < kProbeCap) {
         const uint32_t g0 = h & ~3u;
@@ -646,7 +657,12 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           const uint32_t sl = g0 + (uint32_t)j;
           int32_t k = ks[j];
           if (k == -1) {  // claim it; a lost race leaves the winner's key
+            if (full) {
+              probed = kProbeCap;  // table at its load limit: overflow
+              break;
+            }
             const int32_t old = atomicCAS(&s_hkey[sl], -1, target);
+            if (kLimit && old == -1) (void)atomicAdd(&s_hcount, 1);  // non-returning
             k = old == -1 ? target : old;
           }
           if (k == target) {
@@ -1054,25 +1070,35 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
 
     mark(2);
     // ---- output ------------------------------------------------------------
-    // hash mode: fold overflow entries whose key also reached the LDS table
-    // (a key can straddle the load limit) into the LDS entry
+    // hash mode: the overflow entries leave the HBM hash for a compact
+    // per-workgroup list — key in touched[k] (which held its slot), value in
+    // ov_list[k] — so the selection passes read them coalesced instead of
+    // through two dependent reads per entry and pass, and their slots are
+    // cleared right here for the next source.  A key that also reached the
+    // LDS table (a racing load-limit read lets it into both) is folded into
+    // its LDS entry first; it sits in its first kTsProbeCap slots there.
     const int nov = LDS_ROW ? 0 : min((int64_t)s_ntouch, A.touch_cap * 3 / 4);
     if (!LDS_ROW && nov > 0) {
+      const int fold_cap = (kGwDiag && (A.diag & 512)) ? HASH_SLOTS : kTsProbeCap;
       for (int k = tid; k < nov; k += BLOCK) {
         const int32_t slot = touched[k];
         const int32_t key = __hip_atomic_load(&ov_key[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        double v = __hip_atomic_load(&ov_val[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ov_key[slot], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ov_val[slot], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t h = H::slot(key);
-        for (int probe = 0; probe < HASH_SLOTS; ++probe) {
+        for (int probe = 0; probe < fold_cap; ++probe) {
           const int32_t kk = s_hkey[h];
           if (kk == -1) break;
           if (kk == key) {
-            const double v = __hip_atomic_load(&ov_val[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             atomicAdd(&s_hval[h], v);
-            __hip_atomic_store(&ov_val[slot], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v = 0.0;
             break;
           }
           h = H::next(h);
         }
+        touched[k] = key;
+        ov_list[k] = v;
       }
       __syncthreads();
     }
@@ -1145,10 +1171,9 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       } else if (idx < NL) {
         *id = s_hkey[idx];
         *val = s_hval[idx];
-      } else {
-        const int32_t slot = touched[idx - NL];
-        *id = __hip_atomic_load(&ov_key[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *val = __hip_atomic_load(&ov_val[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {  // the compact overflow list (relaxed atomic loads: plain ones here trip a gfx950 codegen bug)
+        *id = __hip_atomic_load(&touched[idx - NL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *val = __hip_atomic_load(&ov_list[idx - NL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return *val > 0.0;
     };
@@ -1433,11 +1458,6 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
             s_hkey[tid + i * BLOCK] = -1;
           }
       }
-      for (int k = tid; k < nov; k += BLOCK) {
-        const int32_t slot = touched[k];
-        __hip_atomic_store(&ov_key[slot], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ov_val[slot], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
     }
     __syncthreads();
     if (tid == 0) {
@@ -1648,6 +1668,7 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   ws_free(t.spawn_first);
   ws_free(t.spawn_mass);
   ws_free(t.acc_row);
+  ws_free(t.ov_list);
   ws_free(t.ov_keys);
   ws_free(t.touched);
   ws_free(t.enum_tgt);
@@ -1712,7 +1733,7 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   const int64_t enum_cap = pipe ? (int64_t)step * level_cap : 1;
   const int64_t per_block = nb * ((int64_t)(L + 1) * level_cap * 20 + spawn_cap * 20 + 4) + 2 * level_cap * 8 +
                             (level_cap + 1) * 4 + (pipe ? 2 * enum_cap * 12 : 0) +
-                            (lds_row ? 0 : touch_cap * 16) + (pipe ? TOPK_MAX * 12 : 0);
+                            (lds_row ? 0 : touch_cap * 24) + (pipe ? TOPK_MAX * 12 : 0);
   int dev_cus = 256;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, g->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
@@ -1747,7 +1768,8 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
     GW_HIP_TRY(hipGetLastError());
   }
   if (!lds_row) {
-    if ((rc = ws_alloc(g, &t.acc_row, blocks * touch_cap)) || (rc = ws_alloc(g, &t.ov_keys, blocks * touch_cap)))
+    if ((rc = ws_alloc(g, &t.acc_row, blocks * touch_cap)) || (rc = ws_alloc(g, &t.ov_keys, blocks * touch_cap)) ||
+        (rc = ws_alloc(g, &t.ov_list, blocks * touch_cap)))
       return rc;
     GW_HIP_TRY(hipMemset(t.acc_row, 0, sizeof(double) * blocks * touch_cap));
     GW_HIP_TRY(hipMemset(t.ov_keys, 0xFF, sizeof(int32_t) * blocks * touch_cap));  // -1 = empty
@@ -1818,6 +1840,7 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   A.spawn_mass = t.spawn_mass;
   A.ov_keys = t.ov_keys;
   A.ov_vals = t.acc_row;
+  A.ov_list = t.ov_list;
   A.enum_tgt = t.enum_tgt;
   A.enum_val = t.enum_val;
   A.enum_cap = t.enum_cap;
