@@ -547,243 +547,6 @@ k_walk_scale(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t wal
   }
 }
 
-// The second-order rejection sampler on an unweighted undirected graph with
-// slot entries and neighbour hash sets (GW_N2V_REJECTION: config 2's one-shot
-// sampler, config 4, the north-star graph): k_walk_scale's draws and
-// decisions — the walks are identical — restructured so that every loop
-// iteration is ONE memory round trip for the wave.
-//
-// k_walk_scale reads a candidate's slot entry and then, for the lanes whose
-// decision needs has_edge, probes a neighbour hash in the same iteration:
-// two dependent round trips (more for linear-probing runs), and every lane of
-// the wave waits for them (R-MAT-20 p=0.25 q=4: 1.98 trials and 3.1 fabric
-// requests per step, 72% of the calibrated request rate — the requests are
-// fine, the chains are not).  Here a candidate that needs a probe is parked
-// and its probe (one 16 B bucket, gw_eh_has) is issued in the NEXT iteration
-// together with the entry of the step's next trial, drawn speculatively: the
-// probe rejects most candidates (q = 4: ~90% of the prev-branch ones), and
-// then that entry is exactly the next trial's; when the probe accepts, the
-// walker moves to the parked candidate and the speculative entry is dropped.
-// Every draw keeps its (seed, walk, step, trial) key, so the walk does not
-// depend on the pipelining; trial counters count the evaluated trials only.
-//
-// MIX (q > 1): the mixture proposal of k_walk_scale when deg(prev) < deg(cur)
-// (a prev-branch candidate is parked for "x in N(cur)"), the uniform proposal
-// otherwise (parked for "x in N(prev)").  !MIX (q < 1; q = 1 never probes):
-// the uniform proposal, whose probes mostly ACCEPT (a candidate passes unless
-// it is a common neighbour), so a parked probe is issued alone.
-template <bool MIX>
-__global__ void __launch_bounds__(kBlock)
-k_walk_rej(gw_dev_graph G, N2VParams P, int L, int64_t walk_begin, int64_t walk_count, int shuffle,
-           int32_t* __restrict__ out, int32_t* __restrict__ lens, unsigned long long* __restrict__ counters) {
-  __shared__ int32_t s_stage[kBlock / 64][kStage][64];
-  __shared__ int32_t s_ids[kBlock / 64][64];
-  const int lane = threadIdx.x & 63;
-  int32_t* stage = &s_stage[threadIdx.x >> 6][0][lane];
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = i < walk_count;
-  unsigned long long my_steps = 0, my_trials = 0;
-  const int64_t w = walk_begin + (valid ? i : 0);
-  const uint32_t c0 = (uint32_t)w, c1 = (uint32_t)((uint64_t)w >> 32);
-  int32_t cur = -1, prev = -1;
-  int64_t b = 0, pb = 0;  // rows of cur and prev: (first slot, degree)
-  int32_t dc = 0, dpv = 0;
-  int len = L;
-  uint32_t trial = 0;  // trials drawn in this step (a parked candidate's included)
-  // parked candidate: 0 none, 1 probe x in N(prev), 2 probe x in N(cur)
-  uint32_t park = 0u;
-  int32_t px = 0, pnd = 0;
-  int64_t pnb = 0;
-  if (valid) {
-    const uint64_t it = (uint64_t)w / (uint64_t)G.n;
-    const uint64_t pos = (uint64_t)w % (uint64_t)G.n;
-    const uint64_t sp = shuffle ? gw_feistel_perm(pos, (uint64_t)G.n, P.pk0, P.pk1, (uint32_t)it) : pos;
-    cur = G.order[sp];
-    len = 1;
-    b = G.offsets[cur];
-    dc = (int32_t)(G.offsets[cur + 1] - b);
-  }
-  stage[0] = cur;
-  const bool vec_ok = (L & 3) == 0;
-  for (;;) {
-    const bool active = len < L && dc != 0;
-    if (__ballot(active) == 0ull) break;
-    bool ready = false;
-    int flen = 0;
-    // ---- this iteration's reads, issued together: the parked candidate's
-    // bucket and the entry of the (possibly speculative) next trial
-    const int64_t d = dc;
-    uint32_t hs = 0u;
-    int64_t hrb = 0;
-    uint32_t hnb = 0u;
-    if (active && park) {
-      hrb = park == 1u ? pb : b;
-      hnb = (uint32_t)(park == 1u ? dpv : dc);
-      hs = gw_eh_slot(px, hnb);
-    }
-    int64_t slot = -1;      // candidate slot (-1: return-edge outlier, no read)
-    bool from_cur = true;   // mixture branch of the candidate
-    double t = 0.0;         // uniform proposal: the acceptance draw scaled by M
-    double um = 0.0;        // mixture: u.w (acceptance of prev drawn from N(cur))
-    // speculate the next trial beside a parked probe only where probes mostly
-    // reject (q > 1: the candidate must be a common neighbour); at q < 1 a
-    // probed candidate is accepted unless it is common, so the speculative
-    // entry would mostly be dropped: the probe goes alone
-    const bool draw = active && (MIX || !park);
-    if (draw) {
-      if (len == 1) {  // first order (node2vec.py:28-29)
-        const gw_u4 u = gw_philox(c0, c1, 1u, 0u, P.k0, P.k1);
-        slot = b + (int64_t)gw_index(u.x, u.z, (uint32_t)d);
-      } else {
-        const gw_u4 u = gw_philox(c0, c1, (uint32_t)len, trial, P.k0, P.k1);
-        if (MIX && dpv < dc) {
-          const int64_t dp = dpv;
-          const double Ac = (double)d * P.a_q;
-          const double H = P.mix_o + Ac + (double)dp * P.mix_p;
-          const double r = gw_u01(u.z) * H;
-          if (r >= P.mix_o) {
-            from_cur = r < P.mix_o + Ac;
-            slot = (from_cur ? b : pb) + (int64_t)gw_index(u.x, u.y, (uint32_t)(from_cur ? d : dp));
-            um = gw_u01(u.w);
-          }
-        } else {
-          const double A = P.M * (double)d + P.extra;  // undirected: the return edge always exists, weight 1
-          if (!(P.extra > 0.0 && gw_u01(u.z) * A < P.extra)) {
-            slot = b + (int64_t)gw_index(u.x, u.y, (uint32_t)d);
-            t = gw_u01(u.w) * P.M;
-          }
-        }
-      }
-    }
-    int4 hv = make_int4(-1, -1, -1, -1);
-    uint4 ev = make_uint4(0u, 0u, 0u, 0u);
-    if (active && park) hv = gw_eh_row(G.eh, hrb)[hs];
-    if (slot >= 0) ev = *reinterpret_cast<const uint4*>(G.sent + slot);
-    if (active) {
-      bool acc = false;
-      int32_t next = prev;     // the outlier's target
-      int64_t nb = pb;
-      int32_t nd = dpv;  // row of next
-      bool drawn = draw;       // this iteration's draw is evaluated (not dropped)
-      if (park) {
-        const int r0 = gw_eh_scan(hv, px);
-        const bool adj = r0 > 0 || (r0 < 0 && gw_eh_has_from(G.eh, hrb, hnb, hs, px));
-        // uniform proposal past t >= min(1, 1/q): accepted iff common (q > 1) / not common (q < 1)
-        const bool a = park == 2u ? adj : ((P.a_q < 1.0) ? adj : !adj);
-        park = 0u;
-        if (a) {
-          acc = true;
-          drawn = false;  // the speculative draw is dropped
-          next = px;
-          nb = pnb;
-          nd = pnd;
-        }
-      }
-      if (drawn) {
-        ++trial;
-        if (slot >= 0) {
-          next = (int32_t)ev.x;
-          nd = (int32_t)ev.y;
-          nb = (int64_t)((uint64_t)ev.z | ((uint64_t)ev.w << 32));
-        }
-        bool needs = false;  // decided by a probe next iteration
-        if (len == 1) {
-          acc = true;
-        } else if (MIX && dpv < dc) {
-          if (slot < 0) {
-            acc = true;  // return-edge outlier
-          } else if (from_cur) {
-            acc = next != prev || um < P.mix_prev;
-            if (trial >= (1u << 24)) acc = true;
-          } else if (next != prev) {
-            needs = true;  // x in N(cur)?
-          }
-          if (needs) park = 2u;
-        } else {
-          if (slot < 0) {
-            acc = true;  // return-edge outlier
-          } else if (next == prev) {
-            acc = t < P.h_prev;
-          } else if (t < P.lo) {
-            acc = true;
-          } else {
-            needs = true;  // x in N(prev)?
-            park = 1u;
-          }
-          if (trial >= (1u << 24)) {
-            acc = true;
-            park = 0u;
-          }
-        }
-        if (park) {
-          px = next;
-          pnb = nb;
-          pnd = nd;
-        }
-      }
-      if (acc) {
-        my_trials += trial;
-        trial = 0;
-        prev = cur;
-        pb = b;
-        dpv = dc;
-        cur = next;
-        b = nb;  // from the slot entry, or prev's row after an outlier return
-        dc = nd;
-        stage[64 * (len & (kStage - 1))] = cur;
-        ready = (len & (kStage - 1)) == kStage - 1;
-        flen = len;
-        ++len;
-      }
-    }
-    // flush (k_walk_scale's cooperative, compacted flush)
-    const unsigned long long rm = __ballot(ready);
-    if (rm && !(kGwDiag && P.diag)) {
-      if (vec_ok) {
-        const int nready = __popcll(rm);
-        int32_t* ids = s_ids[threadIdx.x >> 6];
-        __builtin_amdgcn_wave_barrier();
-        if (ready)
-          ids[__builtin_amdgcn_mbcnt_hi((uint32_t)(rm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rm, 0u))] = lane;
-        __builtin_amdgcn_wave_barrier();
-        const int32_t* sw = &s_stage[threadIdx.x >> 6][0][0];
-        for (int j = 0; 16 * j < nready; ++j) {
-          const int q = 16 * j + (lane >> 2), p4 = 4 * (lane & 3);
-          const int r = ids[q < nready ? q : nready - 1];
-          const int lr = __shfl(flen, r, 64);
-          const int64_t ir = ((int64_t)__shfl((int)(i >> 32), r, 64) << 32) | (uint32_t)__shfl((int)i, r, 64);
-          if (q < nready) {
-            const int4 v = make_int4(sw[64 * p4 + r], sw[64 * (p4 + 1) + r], sw[64 * (p4 + 2) + r], sw[64 * (p4 + 3) + r]);
-            *reinterpret_cast<int4*>(out + ir * (int64_t)L + (lr - (kStage - 1)) + p4) = v;
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-      } else if (ready) {
-        int32_t* dst = out + i * (int64_t)L + (flen - (kStage - 1));
-        for (int j = 0; j < kStage; ++j) dst[j] = stage[64 * j];
-      }
-    }
-  }
-  if (valid) {
-    int32_t* row = out + i * (int64_t)L;
-    const int base = len & ~(kStage - 1);
-    for (int tt = base; tt < len; ++tt) row[tt] = stage[64 * (tt - base)];
-    for (int tt = len; tt < L; ++tt) row[tt] = -1;
-    if (lens) lens[i] = len;
-    my_steps = (unsigned long long)(len - 1);
-  }
-  if (counters) {
-    for (int off = 32; off > 0; off >>= 1) {
-      my_steps += __shfl_down(my_steps, off, 64);
-      my_trials += __shfl_down(my_trials, off, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-      atomicAdd(&counters[0], my_steps);
-      atomicAdd(&counters[1], my_trials);
-    }
-  }
-}
-
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1303,13 +1066,6 @@ int gw_dev_n2v_walks(gw_graph* g, int L, uint64_t seed, int64_t walk_begin, int6
   } else if (wt) {
     if (di) GW_LAUNCH(false, true, true);
     else GW_LAUNCH(false, true, false);
-  } else if (!di && g->d.sent && g->d.eh && P.a_q > 1.0 && !(kGwDiag && GW_DIAG_ENV("GW_DIAG_REJ_SCALE"))) {
-    // q < 1: a parked probe per iteration (k_walk_rej); GW_DIAG_REJ_SCALE: k_walk_scale (A/B, same walks)
-    k_walk_rej<false><<<grid, kBlock, 0, s>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev, len_dev, C);
-  } else if (kGwDiag && !di && g->d.sent && g->d.eh && P.a_q < 1.0 && GW_DIAG_ENV("GW_DIAG_REJ_PIPE")) {
-    // q > 1: k_walk_scale's mixture kernel is the shipped one (round 5: with the bucketed neighbour hash it runs
-    // at the calibrated request rate, and the parked probe + speculative trial only adds requests); A/B only
-    k_walk_rej<true><<<grid, kBlock, 0, s>>>(g->d, P, L, walk_begin, walk_count, shuffle, out_dev, len_dev, C);
   } else {
     if (di) GW_LAUNCH(false, false, true);
     else if (P.a_q < 1.0) GW_LAUNCH_MIX(false, false, false, true);  // q > 1: mixture proposal

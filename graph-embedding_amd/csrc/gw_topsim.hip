@@ -50,8 +50,8 @@ struct TsArgs {
   int variant;
   int diag;  // GW_DIAG_TS (timing experiments only, wrong results): 1 = walkers skip computePathSim, 2 = cheap RNG,
              // 4 / 8 = walker reads confined to the first 2^26 / 2^27 slot entries;
-             // A/B knobs (same results): 32 = no deferred ordering, 512 = new LDS-hash keys reserved on a shared
-             // load counter (round 4), 1024 = a walker's pair update before its next entry load (round 4),
+             // A/B knobs (same results): 32 = no deferred ordering, 8192 = counter-free LDS-hash insert (4-wide
+             // probes, kTsProbeCap), 1024 = a walker's pair update before its next entry load (round 4),
              // 2048 = a walker's last pair update not carried into the lane's next walker
   int sample;
   double sampled;
@@ -622,47 +622,30 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       return;
     }
     uint32_t h = H::slot(target);
-    // A new key claims an empty slot with one CAS, once a plain read of the
-    // workgroup's load counter says the table is below HASH_LIMIT (75%), and
-    // then bumps the counter with a non-returning LDS add; a key whose first
-    // kTsProbeCap slots are taken, or that finds the table at its limit, goes
-    // to the HBM overflow hash.  (Round 4 reserved every new key with a
-    // RETURNING add on the shared counter first — P10M sources insert ~2,700
-    // new keys per ~2,870 updates, so the counter serialised nearly every
-    // update; diag bit 512 restores it.  With no limit at all, diag bit 8192,
-    // a table that fills up — arxiv at SAMPLE 10000, the P10M stretch — makes
-    // every new key walk the whole cap.)  Slots are never freed while a
-    // source accumulates, so a key's chain never changes: a key is in its
-    // first kTsProbeCap slots or in the overflow hash; the rare key that a
-    // racing counter read lets into both is folded before selection.
-    // The keys are read four at a time (one ds_read_b128 of the aligned
-    // group holding the probe position): a chain of up to 16 slots costs at
-    // most five LDS reads.
-    if (!(kGwDiag && (A.diag & 512))) {
-      // the table at its load limit (read once per update): no more claims.
-      // (pipelined STEP >= 5 kernels go without the limit: at 125 of 128 VGPRs the
-      // extra live state spills 40 B in k_topsim_pipe<5>.)
-      constexpr bool kLimit = STEP < 5 || !PIPE;
-      const bool full = kLimit && !(kGwDiag && (A.diag & 8192)) && *(volatile int*)&s_hcount >= HASH_LIMIT;
-      constexpr int kProbeCap = kTsProbeCap;
+    // Linear probing from the key's slot; a new key first reserves an entry on
+    // the workgroup's load counter, so the table stays below HASH_LIMIT (75%)
+    // and every chain ends at an empty slot within a few probes; past the
+    // limit new keys go to the HBM overflow hash.  Measured against it in one
+    // library (round 5, profiles/r05/tsab_r05e_knobs.jsonl, diag bit 8192): a
+    // counter-free insert (a CAS on the empty slot, keys read four at a time,
+    // at most kTsProbeCap slots) is +1.2% on P10M and +6.8% on arxiv at SAMPLE
+    // 10000, whose tables fill; with an approximate limit (a plain counter
+    // read and a non-returning add) +3.7% / +7.4%.  (Round 4 measured the
+    // counter-free insert at -2.4% before the fold and output changes.)
+    if (kGwDiag && (A.diag & 8192)) {
       int probed = 0;
-      while (probed < kProbeCap) {
+      while (probed < kTsProbeCap) {
         const uint32_t g0 = h & ~3u;
         const int4 kv = *reinterpret_cast<const int4*>(&s_hkey[g0]);
         const int32_t ks[4] = {kv.x, kv.y, kv.z, kv.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if ((uint32_t)j < (h & 3u) || probed >= kProbeCap) continue;
+          if ((uint32_t)j < (h & 3u) || probed >= kTsProbeCap) continue;
           ++probed;
           const uint32_t sl = g0 + (uint32_t)j;
           int32_t k = ks[j];
           if (k == -1) {  // claim it; a lost race leaves the winner's key
-            if (full) {
-              probed = kProbeCap;  // table at its load limit: overflow
-              break;
-            }
             const int32_t old = atomicCAS(&s_hkey[sl], -1, target);
-            if (kLimit && old == -1) (void)atomicAdd(&s_hcount, 1);  // non-returning
             k = old == -1 ? target : old;
           }
           if (k == target) {
@@ -1079,7 +1062,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     // its LDS entry first; it sits in its first kTsProbeCap slots there.
     const int nov = LDS_ROW ? 0 : min((int64_t)s_ntouch, A.touch_cap * 3 / 4);
     if (!LDS_ROW && nov > 0) {
-      const int fold_cap = (kGwDiag && (A.diag & 512)) ? HASH_SLOTS : kTsProbeCap;
+      // (counter-limited table: the chain ends at an empty slot; diag 8192: within kTsProbeCap slots)
+      const int fold_cap = (kGwDiag && (A.diag & 8192)) ? kTsProbeCap : HASH_SLOTS;
       for (int k = tid; k < nov; k += BLOCK) {
         const int32_t slot = touched[k];
         const int32_t key = __hip_atomic_load(&ov_key[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
