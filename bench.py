@@ -883,7 +883,7 @@ TOPSIM_GRAPHS = {"blog": ("blog.txt", 10313, ",", "lshrank blog, V=10313, 333,98
                  "moreno": ("moreno_crime_crime.txt", 1380, "\t", "lshrank moreno, V=1380, 1,476 edges")}
 
 
-def topsim_roofline(ext, upd, kt, tag, nsrc, nnz, step):
+def topsim_roofline(ext, upd, kt, tag, nsrc, nnz, step, n=None):
     """52 B per path extension + 24 B per pair-update / kernel time.
     The denominator follows where the data lives: the slot table (16 B per
     adjacency entry) and the level records of lshrank graphs stay in the 256 MB
@@ -905,7 +905,10 @@ def topsim_roofline(ext, upd, kt, tag, nsrc, nnz, step):
             "traffic": prof["hbm_bytes_per_launch"] if prof else None,
             "traffic_GBps": prof["hbm_bytes_per_launch"] / kt / 1e9 if prof else None,
             "algorithmic_bytes": alg, "slot_table_bytes": table, "kernel": "k_topsim", "kernel_ms": kt * 1e3,
-            "units_per_launch": nsrc, "pmc_tag": tag, "pmc_match": {"kernel": f"k_topsim(_2wg|_pipe|_pipe_row)?<{step}[,>]", "grid": None},
+            "units_per_launch": nsrc, "pmc_tag": tag,
+            # dense-row (lshrank) and hash-mode (P10M) kernels are told apart by name, STEP by the template argument
+            "pmc_match": {"kernel": (f"k_topsim(_pipe_row)?<{step}[,>]" if n is not None and n * 8 <= 96 * 1024
+                                     else f"k_topsim(_2wg|_pipe)<{step}[,>]"), "grid": None},
             "random_line_roofline": line_roofline(prof, kt, table, 128)}
 
 
@@ -928,7 +931,7 @@ def p10m_graph(R, args):
     return _P10M_GRAPH[key]
 
 
-def run_topsim(R, args, name, sample=None, step=None, stride=1):
+def run_topsim(R, args, name, p10m_sample=None, p10m_step=None, stride=1):
     """TopSim_singleSample: lshrank graphs (config 3; every rank all sources) or
     P10M (config 5 at SAMPLE 1000 / STEP 3, or the SURVEY §8d stretch
     SAMPLE 10000 / STEP 5; sources split over ranks, strong scaling)."""
@@ -972,7 +975,7 @@ def run_topsim(R, args, name, sample=None, step=None, stride=1):
         srcs = srcs_all[rank::world]
         desc = (f"{args.p10m_vertices} vertices, {10 * args.p10m_vertices} R-MAT lines, {len(srcs_all)} non-isolated "
                 f"sources" + (f" (every {stride}th)" if stride > 1 else "") + f" split round-robin over {world} rank(s)")
-        K, sample, step = 100, sample or 1000, step or 3
+        K, sample, step = 100, p10m_sample or 1000, p10m_step or 3
         scaling = "strong"
         keep = pg
     else:
@@ -1045,7 +1048,7 @@ def run_topsim(R, args, name, sample=None, step=None, stride=1):
         "config": {"workload": f"TopSim_singleSample on {name} ({desc}, Java multigraph)",
                    "step": step, "sample": sample, "C": 0.6, "topk": K},
         "pair_updates": upd, "path_extensions": ext, "seconds": tel, "cpu_baseline": cpu_ts, "allgather": gather,
-        "roofline": topsim_roofline(ext_l, upd_l, kms * 1e-3, tag, nloc, int(offs[-1]), step),
+        "roofline": topsim_roofline(ext_l, upd_l, kms * 1e-3, tag, nloc, int(offs[-1]), step, len(offs) - 1),
     }
 
 

@@ -674,7 +674,7 @@ static bool listed_pays(gw_graph* g, double q) {
 // bitset walk time per step (R-MAT-20 headline 3.2e10 walk-steps/s) and the
 // rejection sampler's time per trial (see n2v_prepare_auto)
 constexpr double kBitsetStepSeconds = 1.0 / 3.2e10;
-constexpr double kRejTrialSeconds = 4.0e-11;
+constexpr double kRejTrialSeconds = 3.0e-11;  // round 5 (bucketed neighbour hash); round 4: 4.0e-11
 
 // GW_N2V_AUTO: see include/graphwalk.h
 static int n2v_prepare_auto(gw_graph* g, double p, double q) {
@@ -706,10 +706,10 @@ static int n2v_prepare_auto(gw_graph* g, double p, double q) {
   };
   // pilot: the rejection sampler's own walks (65,536 walks of length 80 from
   // iteration 0's shuffled starts, a fixed internal seed) counting its trials
-  // per step; the modelled time per trial is measured (round 4, mixture
-  // proposal at q > 1: R-MAT-20 p = 0.25 q = 4: 1.98 trials/step, 39.4 ms per
-  // 5.1e8 steps; R-MAT-24 ef 6: 2.20, 53.9 ms per 5.4e8; R-MAT-24 ef 16 p = 1
-  // q = 0.5: 1.03, 273 ms per 7.0e9).  Counting, not timing, keeps the choice
+  // per step; the modelled time per trial is measured (round 5, bucketed
+  // neighbour hash: R-MAT-20 p = 0.25 q = 4: 1.98 trials/step, 28.3 ms per
+  // 5.1e8 steps = 2.8e-11 s per trial; R-MAT-24 ef 16 p = 1 q = 0.5: 1.045,
+  // 25.8 ms per 7.0e8 = 3.5e-11).  Counting, not timing, keeps the choice
   // (and so the walks) a function of the inputs.
   const int64_t pw = std::min<int64_t>(65536, std::max<int64_t>(g->n, 1));
   const int L = 80;
