@@ -115,9 +115,8 @@ struct gw_topsim_ws {
   int32_t* spawn_level = nullptr; // [blocks][spawn_cap]
   int32_t* spawn_first = nullptr; // [blocks][spawn_cap+1] walker prefix
   double* spawn_mass = nullptr;   // [blocks][spawn_cap] child mass m/ceil(m)
-  double* acc_row = nullptr;      // [blocks][touch_cap] overflow hash values (hash mode)
+  double* acc_row = nullptr;      // [blocks][touch_cap] overflow hash, 16 B slots {int32 key (-1 empty), pad, f64 value}
   double* ov_list = nullptr;      // [blocks][touch_cap] compacted overflow values of a source (hash mode)
-  int32_t* ov_keys = nullptr;     // [blocks][touch_cap] overflow hash keys (-1 empty)
   int32_t* touched = nullptr;     // [blocks][touch_cap] claimed overflow slots
   int pipe = 0;                   // pipelined kernel (levels of the next source built by wave 0 during
                                   // the walkers): level / spawner scratch doubled per workgroup

@@ -586,7 +586,6 @@ void gw_dev_release(gw_graph* g) {
   dev_free(t.spawn_first);
   dev_free(t.acc_row);
   dev_free(t.ov_list);
-  dev_free(t.ov_keys);
   dev_free(t.touched);
   dev_free(t.enum_tgt);
   dev_free(t.enum_val);

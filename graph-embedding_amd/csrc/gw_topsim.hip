@@ -77,7 +77,6 @@ struct TsArgs {
   int32_t* spawn_level;
   int32_t* spawn_first;
   double* spawn_mass;
-  int32_t* ov_keys;
   double* ov_vals;
   double* ov_list;  // [blocks][touch_cap] the compacted overflow values of a source (keys in `touched`)
   int32_t* enum_tgt;  // pipelined kernel: enumerated-node pair updates of a source, [blocks][2][enum_cap]
@@ -562,8 +561,11 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   // per-workgroup HBM overflow hash (large n)
   double* s_hval = s_row;                                   // [HASH_SLOTS]
   int32_t* s_hkey = reinterpret_cast<int32_t*>(s_row + HASH_SLOTS);  // [HASH_SLOTS]
-  int32_t* ov_key = LDS_ROW ? nullptr : (A.ov_keys + blk * A.touch_cap);
-  double* ov_val = LDS_ROW ? nullptr : (A.ov_vals + blk * A.touch_cap);
+  // overflow hash slots are 16 B {int32 key, pad, f64 value}: the CAS on the
+  // key and the add to the value touch ONE cache line (round 5; two separate
+  // arrays before); key of slot h at ov_key[4h], value at ov_val[2h + 1]
+  int32_t* ov_key = LDS_ROW ? nullptr : reinterpret_cast<int32_t*>(A.ov_vals + 2 * blk * A.touch_cap);
+  double* ov_val = LDS_ROW ? nullptr : (A.ov_vals + 2 * blk * A.touch_cap);
   double* ov_list = LDS_ROW ? nullptr : (A.ov_list + blk * A.touch_cap);
   int32_t* touched = LDS_ROW ? nullptr : (A.touched + blk * A.touch_cap);
   const uint32_t ov_mask = (uint32_t)(A.touch_cap - 1);
@@ -600,14 +602,14 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   auto ov_add = [&](int32_t target, double val) {
     uint32_t h = ((uint32_t)target * 0x9E3779B1u) & ov_mask;
     for (int64_t probe = 0; probe <= (int64_t)ov_mask; ++probe) {
-      const int32_t old = atomicCAS(&ov_key[h], -1, target);
+      const int32_t old = atomicCAS(&ov_key[4 * h], -1, target);
       if (old == -1 || old == target) {
         if (old == -1) {
           const int k = atomicAdd(&s_ntouch, 1);
           if ((int64_t)k < A.touch_cap * 3 / 4) touched[k] = (int32_t)h;
           else atomicOr(A.error_flag, 2);
         }
-        atomicAdd(&ov_val[h], val);
+        atomicAdd(&ov_val[2 * h + 1], val);
         return;
       }
       h = (h + 1) & ov_mask;
@@ -1064,25 +1066,47 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     if (!LDS_ROW && nov > 0) {
       // (counter-limited table: the chain ends at an empty slot; diag 8192: within kTsProbeCap slots)
       const int fold_cap = (kGwDiag && (A.diag & 8192)) ? kTsProbeCap : HASH_SLOTS;
-      for (int k = tid; k < nov; k += BLOCK) {
-        const int32_t slot = touched[k];
-        const int32_t key = __hip_atomic_load(&ov_key[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        double v = __hip_atomic_load(&ov_val[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ov_key[slot], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ov_val[slot], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t h = H::slot(key);
-        for (int probe = 0; probe < fold_cap; ++probe) {
-          const int32_t kk = s_hkey[h];
-          if (kk == -1) break;
-          if (kk == key) {
-            atomicAdd(&s_hval[h], v);
-            v = 0.0;
-            break;
-          }
-          h = H::next(h);
+      // four entries per thread and round, their slot reads issued together
+      // (the stretch compacts ~31k entries per source: the loop was a chain of
+      // dependent random reads per entry)
+      constexpr int U = 4;
+      for (int k0 = tid; k0 < nov; k0 += U * BLOCK) {
+        int32_t slot[U], key[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int k = k0 + u * BLOCK;
+          slot[u] = k < nov ? __hip_atomic_load(&touched[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : -1;
         }
-        touched[k] = key;
-        ov_list[k] = v;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          key[u] = -1;
+          v[u] = 0.0;
+          if (slot[u] >= 0) {
+            key[u] = __hip_atomic_load(&ov_key[4 * slot[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[u] = __hip_atomic_load(&ov_val[2 * slot[u] + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (slot[u] < 0) continue;
+          __hip_atomic_store(&ov_key[4 * slot[u]], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&ov_val[2 * slot[u] + 1], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          uint32_t h = H::slot(key[u]);
+          for (int probe = 0; probe < fold_cap; ++probe) {
+            const int32_t kk = s_hkey[h];
+            if (kk == -1) break;
+            if (kk == key[u]) {
+              atomicAdd(&s_hval[h], v[u]);
+              v[u] = 0.0;
+              break;
+            }
+            h = H::next(h);
+          }
+          const int k = k0 + u * BLOCK;
+          __hip_atomic_store(&touched[k], key[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&ov_list[k], v[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
       __syncthreads();
     }
@@ -1653,7 +1677,6 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   ws_free(t.spawn_mass);
   ws_free(t.acc_row);
   ws_free(t.ov_list);
-  ws_free(t.ov_keys);
   ws_free(t.touched);
   ws_free(t.enum_tgt);
   ws_free(t.enum_val);
@@ -1717,7 +1740,7 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   const int64_t enum_cap = pipe ? (int64_t)step * level_cap : 1;
   const int64_t per_block = nb * ((int64_t)(L + 1) * level_cap * 20 + spawn_cap * 20 + 4) + 2 * level_cap * 8 +
                             (level_cap + 1) * 4 + (pipe ? 2 * enum_cap * 12 : 0) +
-                            (lds_row ? 0 : touch_cap * 24) + (pipe ? TOPK_MAX * 12 : 0);
+                            (lds_row ? 0 : touch_cap * 28) + (pipe ? TOPK_MAX * 12 : 0);
   int dev_cus = 256;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, g->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
@@ -1752,11 +1775,11 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
     GW_HIP_TRY(hipGetLastError());
   }
   if (!lds_row) {
-    if ((rc = ws_alloc(g, &t.acc_row, blocks * touch_cap)) || (rc = ws_alloc(g, &t.ov_keys, blocks * touch_cap)) ||
-        (rc = ws_alloc(g, &t.ov_list, blocks * touch_cap)))
+    // overflow hash: 16 B slots {int32 key (-1 = empty), pad, f64 value}
+    if ((rc = ws_alloc(g, &t.acc_row, 2 * blocks * touch_cap)) || (rc = ws_alloc(g, &t.ov_list, blocks * touch_cap)))
       return rc;
-    GW_HIP_TRY(hipMemset(t.acc_row, 0, sizeof(double) * blocks * touch_cap));
-    GW_HIP_TRY(hipMemset(t.ov_keys, 0xFF, sizeof(int32_t) * blocks * touch_cap));  // -1 = empty
+    GW_HIP_TRY(hipMemset(t.acc_row, 0, sizeof(double) * 2 * blocks * touch_cap));
+    GW_HIP_TRY(hipMemset2D(t.acc_row, 16, 0xFF, 4, (size_t)(blocks * touch_cap)));
   }
   t.variant = variant;
   t.sample = sample;
@@ -1822,7 +1845,6 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   A.spawn_level = t.spawn_level;
   A.spawn_first = t.spawn_first;
   A.spawn_mass = t.spawn_mass;
-  A.ov_keys = t.ov_keys;
   A.ov_vals = t.acc_row;
   A.ov_list = t.ov_list;
   A.enum_tgt = t.enum_tgt;
