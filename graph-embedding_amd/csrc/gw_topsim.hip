@@ -1092,16 +1092,26 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           if (slot[u] < 0) continue;
           __hip_atomic_store(&ov_key[4 * slot[u]], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&ov_val[2 * slot[u] + 1], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // the key's LDS chain, four keys per ds_read_b128, up to its first empty slot
           uint32_t h = H::slot(key[u]);
-          for (int probe = 0; probe < fold_cap; ++probe) {
-            const int32_t kk = s_hkey[h];
-            if (kk == -1) break;
-            if (kk == key[u]) {
-              atomicAdd(&s_hval[h], v[u]);
-              v[u] = 0.0;
-              break;
+          bool done = false;
+          for (int probed = 0; probed < fold_cap && !done;) {
+            const uint32_t g0 = h & ~3u;
+            const int4 kv = *reinterpret_cast<const int4*>(&s_hkey[g0]);
+            const int32_t ks[4] = {kv.x, kv.y, kv.z, kv.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              if (done || (uint32_t)j < (h & 3u) || probed >= fold_cap) continue;
+              ++probed;
+              if (ks[j] == -1) {
+                done = true;
+              } else if (ks[j] == key[u]) {
+                atomicAdd(&s_hval[g0 + (uint32_t)j], v[u]);
+                v[u] = 0.0;
+                done = true;
+              }
             }
-            h = H::next(h);
+            h = g0 + 4u == (uint32_t)HASH_SLOTS ? 0u : g0 + 4u;
           }
           const int k = k0 + u * BLOCK;
           __hip_atomic_store(&touched[k], key[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
