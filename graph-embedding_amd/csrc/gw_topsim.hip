@@ -53,8 +53,7 @@ struct TsArgs {
              // A/B knobs (same results): 32 = no deferred ordering, 8192 = counter-free LDS-hash insert (4-wide
              // probes, kTsProbeCap), 1024 = a walker's pair update before its next entry load (round 4),
              // 2048 = a walker's last pair update not carried into the lane's next walker,
-             // 4096 = top-k selection from the compacted LDS table (no register-held values),
-             // 16384 = wave 0's build reads every level back from the level arrays
+             // 4096 = top-k selection from the compacted LDS table (no register-held values)
   int sample;
   double sampled;
   double cache[16];
@@ -336,14 +335,6 @@ __device__ __forceinline__ TsLevelStats ts_wave_levels(const TsArgs& A, int b, i
     __threadfence_block();
     int sz = 1, nsp = 0, nwk = 0, nct = 0;
     bool abort = false;
-    // a level of <= 64 nodes that came out of ONE child chunk stays in the
-    // registers of the lanes that filled it (degree, mass, row offset): the
-    // next level's expansion then skips reading it back through L2 (the
-    // level arrays are still written: walkers and deeper paths read them)
-    bool carried = false;
-    int cd = 0;
-    double cmass = 0.0;
-    int64_t coff = 0;
     // record a pair update (target, val) of lanes with tgt >= 0, queue order irrelevant (a sum)
     auto emit = [&](int32_t tgt, double val) {
       const unsigned long long em = __ballot(tgt >= 0);
@@ -412,15 +403,9 @@ __device__ __forceinline__ TsLevelStats ts_wave_levels(const TsArgs& A, int b, i
         double m = 0.0;
         int64_t o = 0;
         if (j < sz) {
-          if (carried) {
-            d = cd;
-            m = cmass;
-            o = coff;
-          } else {
-            d = Dl[j];
-            m = Ml[j];
-            o = Ol[j];
-          }
+          d = Dl[j];
+          m = Ml[j];
+          o = Ol[j];
         }
         if (d != 0 && m >= (double)d) {  // enumerate (:99)
           cnt = d;
@@ -475,11 +460,6 @@ __device__ __forceinline__ TsLevelStats ts_wave_levels(const TsArgs& A, int b, i
             On[ci] = e.off;
             Pn[ci] = j0 + pl;
             Mn[ci] = cm;
-            if (c0 == 0) {  // candidate carry (used when the level is this one chunk)
-              cd = e.d;
-              cmass = cm;
-              coff = e.off;
-            }
             if (level2 && e.x != s) {  // i = 1: ((mass * C) * deg(mid)) / deg(target) (:183-189)
               tgt = e.x;
               val = ((cm * A.cache[1]) * (double)pd) / (double)e.d;
@@ -493,9 +473,6 @@ __device__ __forceinline__ TsLevelStats ts_wave_levels(const TsArgs& A, int b, i
       if (level2 && nct > A.enum_cap) abort = true;
       if (abort) break;
       if (lane == 0) my_ext += tot;
-      // one parent chunk, one child chunk: lane k holds child k (STEP >= 5: not
-      // carried — at 127 VGPRs the carried level spills 20 B in k_topsim_pipe<5>)
-      carried = STEP < 5 && sz <= 64 && tot <= 64 && !(kGwDiag && (A.diag & 16384));  // 16384: A/B
       sz = tot;
       __threadfence_block();  // the next level is read back from the level arrays
     }
