@@ -1734,7 +1734,8 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   // (wave 0 alone expands the enumerated levels: worth it while they are
   // small next to the walkers — P10M, SAMPLE 1000: ~130 enumerated nodes and
   // ~1,060 walkers per source — not for SAMPLE in the thousands on low-degree
-  // graphs, whose levels reach thousands of nodes)
+  // graphs, whose levels reach thousands of nodes; above kPipeMaxSample the
+  // host replay of the enumerated part decides, pipe_pays_large_sample)
   // The dense LDS row over 72 KB (one workgroup per CU, e.g. blog) runs
   // pipelined at any SAMPLE: its single workgroup otherwise leaves the CU idle
   // of walker reads during every level / output phase (blog, SAMPLE 10000:

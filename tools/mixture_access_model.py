@@ -1,4 +1,4 @@
-"""Where the one-shot rejection sampler's requests go (k_walk_scale, q > 1:
+"""Where the rejection sampler's requests go (k_walk_scale, q > 1:
 the mixture proposal when deg(prev) < deg(cur), the uniform proposal with the
 lazy has_edge probe otherwise).  CPU only.
 
@@ -58,8 +58,7 @@ def N(v):
 
 
 a_p, a_q = 1 / p, 1 / q
-# q < 1 (config 4): the uniform proposal with the lazy probe at every step;
-# k_walk_rej issues a parked probe alone there (no speculative entry)
+# q < 1 (config 4): the uniform proposal with the lazy probe at every step
 mo = max(0.0, a_p - a_q)
 mprev = min(1.0, a_p / a_q)
 M = max(1.0, a_q)
