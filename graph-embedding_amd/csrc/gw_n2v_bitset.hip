@@ -748,7 +748,8 @@ struct BsParams {
   double a_p, a_q;
   uint32_t k0, k1, pk0, pk1;
   uint32_t diag;  // timing experiments only (GW_DIAG_BS): 1 = no select, 2 = no membership test,
-                 // 4 = region blocks / 8 = region words read from a small hot area (wrong walks)
+                 // 4 = region blocks / 8 = region words read from a small hot area (wrong walks),
+                 // 64 = lane-utilisation counters in counters[2..3] (the caller passes 4)
 };
 
 // an arrived entry's kp, c and payload (gw_bs_nbr: packed header when d < 65536)
@@ -831,9 +832,14 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
   uint32_t ph = 0, t = 0;  // phase; select rank (ph 1: j; ph 2: rank inside block g)
   int64_t g = 0;           // region block within the row
   uint32_t dw0 = 0u, dw1 = 0u, kb = 0u;  // ph 1: directory entries g, g+1; ph 3: selected position
+  uint32_t dg_iter = 0, dg_act = 0;  // diag bit 64: wave iterations / this lane's active ones
   for (;;) {
     const bool active = len < L && d != 0;
     if (__ballot(active) == 0ull) break;
+    if (kGwDiag && (P.diag & 64)) {
+      ++dg_iter;
+      dg_act += active ? 1u : 0u;
+    }
     uint32_t slot = 0xFFFFFFFFu;  // entry to fetch (accepted or speculative step)
     bool spec = false;            // slot is accepted unless bit sbit of sw is set
     uint32_t sw = 0u, sbit = 0u;
@@ -1125,6 +1131,14 @@ k_walk_bitset(gw_dev_graph G, BsParams P, int L, int64_t walk_begin, int64_t wal
     if ((threadIdx.x & 63) == 0) {
       atomicAdd(&counters[0], my_steps);
       atomicAdd(&counters[1], my_trials);
+    }
+    if (kGwDiag && (P.diag & 64)) {  // lane utilisation: counters[2] += 64 x wave iterations, [3] += active lanes
+      unsigned long long a = dg_act;
+      for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off, 64);
+      if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&counters[2], 64ull * dg_iter);
+        atomicAdd(&counters[3], a);
+      }
     }
   }
 }
