@@ -63,7 +63,9 @@ def main():
             order = a.libs if rnd % 2 == 0 else list(reversed(a.libs))
             for x in order:
                 out = subprocess.run([sys.executable, os.path.abspath(__file__), x, "--graphs", a.graphs,
-                                      "--reps", str(a.reps)], check=True, stdout=subprocess.PIPE, text=True).stdout
+                                      "--reps", str(a.reps), "--sample", str(a.sample), "--step", str(a.step),
+                                      "--stride", str(a.stride), "--ls-sample", str(a.ls_sample)],
+                                     check=True, stdout=subprocess.PIPE, text=True).stdout
                 for line in out.splitlines():
                     d = json.loads(line)
                     med[(d["graph"], x)].append(d["median_ms"])
