@@ -264,6 +264,7 @@ struct TsPipeMeta {
   long long r;  // index into A.sources
   int s, ds;
   int nspawn, nwalk, ncontrib;
+  uint32_t ovmask;  // slots - 1 of the source's overflow hash (hash mode)
   int valid;
 };
 
@@ -485,6 +486,13 @@ __device__ __forceinline__ TsLevelStats ts_wave_levels(const TsArgs& A, int b, i
       s_pm[b].nspawn = abort ? 0 : nsp;
       s_pm[b].nwalk = abort ? 0 : nwk;
       s_pm[b].ncontrib = abort ? 0 : min(nct, (int)A.enum_cap);
+      // the source's overflow hash (hash mode): pair updates it can make are
+      // STEP per walker + the enumerated ones, so no more distinct overflow
+      // keys; the power of two above 9/8 of that bound (<= touch_cap)
+      const int64_t ub = abort ? 0 : min((int64_t)G.n, (int64_t)nwk * STEP + min(nct, (int)A.enum_cap));
+      int64_t t = 64;
+      while (t < ub + ub / 8 + 1 && t < A.touch_cap) t <<= 1;
+      s_pm[b].ovmask = (uint32_t)(t - 1);
       s_pm[b].valid = 1;
     }
   }
@@ -519,7 +527,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   __shared__ long long s_red[NW];
   __shared__ int s_size[L + 2];
   __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount, s_bin, s_cum, s_exact, s_total,
-      s_ncomp, s_all;
+      s_ncomp, s_all, s_novc;
+  __shared__ uint32_t s_ovmask;  // the slots (minus 1) of this source's overflow hash
   __shared__ unsigned long long s_prefix, s_mask, s_spbase;
   // the output phase's selection arrays share LDS with the levels' child
   // offsets / the walkers' spawner offsets (binary-searched per child / walker)
@@ -569,7 +578,10 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   double* ov_val = LDS_ROW ? nullptr : (A.ov_vals + 2 * blk * A.touch_cap);
   double* ov_list = LDS_ROW ? nullptr : (A.ov_list + blk * A.touch_cap);
   int32_t* touched = LDS_ROW ? nullptr : (A.touched + blk * A.touch_cap);
-  const uint32_t ov_mask = (uint32_t)(A.touch_cap - 1);
+  // the slots a source's overflow hash uses: all touch_cap of them, or (PIPE)
+  // the power of two above the source's own bound on distinct overflow keys,
+  // so that a heavy source's compaction can scan its slots in order
+  // (read from LDS where used: no register held through the walker phase)
   const bool rw = !PIPE && (A.variant == GW_TOPSIM_SINGLE_RW);  // PIPE: TopSim_singleSample only
   const bool enumerate_all = !PIPE && (A.variant == GW_TOPSIM_ENUMERATE);
 
@@ -595,13 +607,16 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   if (tid == 0) {
     s_ntouch = 0;
     s_hcount = 0;
+    s_ovmask = (uint32_t)(A.touch_cap - 1);
   }
   __syncthreads();
 
   // overflow insert into the workgroup's HBM hash (slots claimed by CAS; the
   // claimed slot is recorded for selection and cleanup)
   auto ov_add = [&](int32_t target, double val) {
-    uint32_t h = ((uint32_t)target * 0x9E3779B1u) & ov_mask;
+    // the product's high bits (Fibonacci hashing): clz(mask) = 32 - log2(slots)
+    const uint32_t ov_mask = s_ovmask;  // a power of two >= 2^6, minus 1
+    uint32_t h = ((uint32_t)target * 0x9E3779B1u) >> __builtin_clz(ov_mask);
     for (int64_t probe = 0; probe <= (int64_t)ov_mask; ++probe) {
       const int32_t old = atomicCAS(&ov_key[4 * h], -1, target);
       if (old == -1 || old == target) {
@@ -853,6 +868,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       if (tid == 0) {
         s_wnext = 0u;
         s_ncomp = 0;
+        s_novc = 0;
+        if (!LDS_ROW) s_ovmask = s_pm[cur].ovmask;
       }
       __syncthreads();
     } else {
@@ -860,6 +877,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       s_src = (int)atomicAdd(A.src_counter, 1u);
       s_abort = 0;
       s_ncomp = 0;
+      s_novc = 0;
     }
     __syncthreads();
     r = s_src;
@@ -1063,10 +1081,85 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     // cleared right here for the next source.  A key that also reached the
     // LDS table (a racing load-limit read lets it into both) is folded into
     // its LDS entry first; it sits in its first kTsProbeCap slots there.
-    const int nov = LDS_ROW ? 0 : min((int64_t)s_ntouch, A.touch_cap * 3 / 4);
-    if (!LDS_ROW && nov > 0) {
-      // (counter-limited table: the chain ends at an empty slot; diag 8192: within kTsProbeCap slots)
-      const int fold_cap = (kGwDiag && (A.diag & 8192)) ? kTsProbeCap : HASH_SLOTS;
+    int nov = LDS_ROW ? 0 : min((int64_t)s_ntouch, A.touch_cap * 3 / 4);
+    // (counter-limited table: the chain ends at an empty slot; diag 8192: within kTsProbeCap slots)
+    const int fold_cap = (kGwDiag && (A.diag & 8192)) ? kTsProbeCap : HASH_SLOTS;
+    // the key's LDS chain, four keys per ds_read_b128, up to its first empty slot
+    auto fold_lds = [&](int32_t key, double& v) {
+      uint32_t h = H::slot(key);
+      bool done = false;
+      for (int probed = 0; probed < fold_cap && !done;) {
+        const uint32_t g0 = h & ~3u;
+        const int4 kv = *reinterpret_cast<const int4*>(&s_hkey[g0]);
+        const int32_t ks[4] = {kv.x, kv.y, kv.z, kv.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (done || (uint32_t)j < (h & 3u) || probed >= fold_cap) continue;
+          ++probed;
+          if (ks[j] == -1) {
+            done = true;
+          } else if (ks[j] == key) {
+            atomicAdd(&s_hval[g0 + (uint32_t)j], v);
+            v = 0.0;
+            done = true;
+          }
+        }
+        h = g0 + 4u == (uint32_t)HASH_SLOTS ? 0u : g0 + 4u;
+      }
+    };
+    // a source with many overflow keys for its table (>= 1/8 of the slots)
+    // compacts by scanning the slots in order: coalesced reads and clears
+    // instead of two random line accesses per key through `touched`
+    const uint32_t ov_mask = s_ovmask;
+    const bool ov_scan = !LDS_ROW && nov > 0 && (int64_t)s_ntouch * 8 >= (int64_t)ov_mask + 1 &&
+                         !(kGwDiag && (A.diag & 16384));  // diag bit 16384: always through `touched` (A/B)
+    if (ov_scan) {
+      const int T = (int)ov_mask + 1;
+      const int cap34 = (int)(A.touch_cap * 3 / 4);
+      const int lane = tid & 63;
+      const unsigned long long below = (1ull << lane) - 1ull;
+      constexpr int U = 4;
+      for (int b0 = 0; b0 < T; b0 += U * BLOCK) {
+        int32_t key[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int i = b0 + u * BLOCK + tid;
+          key[u] = -1;
+          v[u] = 0.0;
+          if (i < T) {
+            key[u] = __hip_atomic_load(&ov_key[4 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[u] = __hip_atomic_load(&ov_val[2 * i + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        int cnt[U], pre[U], tot = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const unsigned long long m = __ballot(key[u] != -1);
+          pre[u] = tot + __popcll(m & below);
+          cnt[u] = __popcll(m);
+          tot += cnt[u];
+        }
+        int wbase = 0;
+        if (lane == 0 && tot > 0) wbase = atomicAdd(&s_novc, tot);
+        wbase = __shfl(wbase, 0, 64);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (key[u] == -1) continue;
+          const int i = b0 + u * BLOCK + tid;
+          __hip_atomic_store(&ov_key[4 * i], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&ov_val[2 * i + 1], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          fold_lds(key[u], v[u]);
+          const int k = wbase + pre[u];
+          if (k < cap34) {
+            __hip_atomic_store(&touched[k], key[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ov_list[k], v[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      }
+      __syncthreads();
+      nov = min(s_novc, cap34);
+    } else if (!LDS_ROW && nov > 0) {
       // four entries per thread and round, their slot reads issued together
       // (the stretch compacts ~31k entries per source: the loop was a chain of
       // dependent random reads per entry)
@@ -1093,27 +1186,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           if (slot[u] < 0) continue;
           __hip_atomic_store(&ov_key[4 * slot[u]], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&ov_val[2 * slot[u] + 1], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          // the key's LDS chain, four keys per ds_read_b128, up to its first empty slot
-          uint32_t h = H::slot(key[u]);
-          bool done = false;
-          for (int probed = 0; probed < fold_cap && !done;) {
-            const uint32_t g0 = h & ~3u;
-            const int4 kv = *reinterpret_cast<const int4*>(&s_hkey[g0]);
-            const int32_t ks[4] = {kv.x, kv.y, kv.z, kv.w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              if (done || (uint32_t)j < (h & 3u) || probed >= fold_cap) continue;
-              ++probed;
-              if (ks[j] == -1) {
-                done = true;
-              } else if (ks[j] == key[u]) {
-                atomicAdd(&s_hval[g0 + (uint32_t)j], v[u]);
-                v[u] = 0.0;
-                done = true;
-              }
-            }
-            h = g0 + 4u == (uint32_t)HASH_SLOTS ? 0u : g0 + 4u;
-          }
+          fold_lds(key[u], v[u]);
           const int k = k0 + u * BLOCK;
           __hip_atomic_store(&touched[k], key[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&ov_list[k], v[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1198,10 +1271,14 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     };
     if (A.out_rows) {
       double* orow = A.out_rows + r * (int64_t)n;
+      // (an opaque copy of tid: its row addresses are not hoisted out of the
+      // source loop into a register held through the walker phase)
+      int t0 = tid;
+      asm volatile("" : "+v"(t0));
       if (LDS_ROW) {
-        for (int t = tid; t < n; t += BLOCK) orow[t] = s_row[t];
+        for (int t = t0; t < n; t += BLOCK) orow[t] = s_row[t];
       } else {
-        for (int t = tid; t < n; t += BLOCK) orow[t] = 0.0;
+        for (int t = t0; t < n; t += BLOCK) orow[t] = 0.0;
         __syncthreads();
         for (int idx = tid; idx < NC; idx += BLOCK) {
           int32_t id;
