@@ -587,6 +587,7 @@ void gw_dev_release(gw_graph* g) {
   dev_free(t.acc_row);
   dev_free(t.ov_list);
   dev_free(t.touched);
+  dev_free(t.app);
   dev_free(t.enum_tgt);
   dev_free(t.enum_val);
   dev_free(t.dsel_id);

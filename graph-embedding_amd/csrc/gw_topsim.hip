@@ -53,7 +53,8 @@ struct TsArgs {
              // A/B knobs (same results): 32 = no deferred ordering, 8192 = counter-free LDS-hash insert (4-wide
              // probes, kTsProbeCap), 1024 = a walker's pair update before its next entry load (round 4),
              // 2048 = a walker's last pair update not carried into the lane's next walker,
-             // 4096 = top-k selection from the compacted LDS table (no register-held values)
+             // 4096 = top-k selection from the compacted LDS table (no register-held values),
+             // 16384 = overflow compaction always through `touched`, 32768 = no append-and-reduce path
   int sample;
   double sampled;
   double cache[16];
@@ -86,6 +87,9 @@ struct TsArgs {
   int32_t* dsel_id;  // pipelined kernel, top-k rows: a source's selected entries awaiting order, [blocks][TOPK_MAX]
   double* dsel_val;
   int32_t* touched;
+  double* app;         // pipelined hash mode: [blocks][2][app_cap] 16 B entries (appended, partitioned)
+  int64_t app_cap;     // 0: no append-and-reduce path
+  int64_t heavy_min;   // a source appends past the LDS table when its pair-update bound exceeds this
   unsigned int* src_counter;
   int* error_flag;
   unsigned long long* phase;  // diagnostics (GW_DIAG_TS_PHASES): cycles per phase, thread 0 of each block
@@ -265,6 +269,7 @@ struct TsPipeMeta {
   int s, ds;
   int nspawn, nwalk, ncontrib;
   uint32_t ovmask;  // slots - 1 of the source's overflow hash (hash mode)
+  int heavy;        // append-and-reduce past the LDS table (hash mode)
   int valid;
 };
 
@@ -493,6 +498,7 @@ __device__ __forceinline__ TsLevelStats ts_wave_levels(const TsArgs& A, int b, i
       int64_t t = 64;
       while (t < ub + ub / 8 + 1 && t < A.touch_cap) t <<= 1;
       s_pm[b].ovmask = (uint32_t)(t - 1);
+      s_pm[b].heavy = A.app_cap > 0 && ub > A.heavy_min && ub <= A.app_cap && !(kGwDiag && (A.diag & (32768 | 8192)));
       s_pm[b].valid = 1;
     }
   }
@@ -529,6 +535,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount, s_bin, s_cum, s_exact, s_total,
       s_ncomp, s_all, s_novc;
   __shared__ uint32_t s_ovmask;  // the slots (minus 1) of this source's overflow hash
+  __shared__ int s_heavy, s_napp;  // append-and-reduce source; pair updates appended
+  __shared__ int s_pbase[65], s_pcur[64];  // its partitions' offsets / fill cursors
   __shared__ unsigned long long s_prefix, s_mask, s_spbase;
   // the output phase's selection arrays share LDS with the levels' child
   // offsets / the walkers' spawner offsets (binary-searched per child / walker)
@@ -578,6 +586,20 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   double* ov_val = LDS_ROW ? nullptr : (A.ov_vals + 2 * blk * A.touch_cap);
   double* ov_list = LDS_ROW ? nullptr : (A.ov_list + blk * A.touch_cap);
   int32_t* touched = LDS_ROW ? nullptr : (A.touched + blk * A.touch_cap);
+  // append-and-reduce (PIPE, hash mode): pair updates appended past the LDS
+  // table, then partitioned by key hash into the second buffer
+  // (the block's base offset passes through an empty asm at each use, so it
+  // is recomputed there instead of held in registers through the walkers)
+  // Instantiated for STEP >= 4 only: at STEP 3 (P10M) the pipelined kernel
+  // measured 0.7-1.2% slower with this code present and no source using it
+  // (register allocation), and a STEP-3 source over the LDS table keeps the
+  // HBM hash (profiles/r05/tsab_r05s*, tsab_r05t*).
+  constexpr bool APPEND = PIPE && STEP >= 4;
+  auto app_base = [&](int buf) -> double* {
+    int64_t o = (4 * blk + 2 * buf) * A.app_cap;
+    asm volatile("" : "+s"(o));
+    return A.app + o;
+  };
   // the slots a source's overflow hash uses: all touch_cap of them, or (PIPE)
   // the power of two above the source's own bound on distinct overflow keys,
   // so that a heavy source's compaction can scan its slots in order
@@ -608,6 +630,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     s_ntouch = 0;
     s_hcount = 0;
     s_ovmask = (uint32_t)(A.touch_cap - 1);
+    s_heavy = 0;
+    s_napp = 0;
   }
   __syncthreads();
 
@@ -622,8 +646,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       if (old == -1 || old == target) {
         if (old == -1) {
           const int k = atomicAdd(&s_ntouch, 1);
-          if ((int64_t)k < A.touch_cap * 3 / 4) touched[k] = (int32_t)h;
-          else atomicOr(A.error_flag, 2);
+          if ((int64_t)k >= A.touch_cap * 3 / 4) atomicOr(A.error_flag, 2);
+          else if (!(APPEND && s_heavy)) touched[k] = (int32_t)h;  // (heavy: compacted by the slot scan)
         }
         atomicAdd(&ov_val[2 * h + 1], val);
         return;
@@ -631,6 +655,35 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       h = (h + 1) & ov_mask;
     }
     atomicOr(A.error_flag, 2);
+  };
+
+  // counter-free LDS-hash insert: a CAS on the key's first empty slot, keys
+  // read four at a time, at most kTsProbeCap slots (false: no room)
+  auto cf_insert = [&](int32_t target, double val) -> bool {
+    uint32_t h = H::slot(target);
+    int probed = 0;
+    while (probed < kTsProbeCap) {
+      const uint32_t g0 = h & ~3u;
+      const int4 kv = *reinterpret_cast<const int4*>(&s_hkey[g0]);
+      const int32_t ks[4] = {kv.x, kv.y, kv.z, kv.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if ((uint32_t)j < (h & 3u) || probed >= kTsProbeCap) continue;
+        ++probed;
+        const uint32_t sl = g0 + (uint32_t)j;
+        int32_t k = ks[j];
+        if (k == -1) {  // claim it; a lost race leaves the winner's key
+          const int32_t old = atomicCAS(&s_hkey[sl], -1, target);
+          k = old == -1 ? target : old;
+        }
+        if (k == target) {
+          atomicAdd(&s_hval[sl], val);
+          return true;
+        }
+      }
+      h = g0 + 4u == (uint32_t)HASH_SLOTS ? 0u : g0 + 4u;
+    }
+    return false;
   };
 
   // accumulate one pair update
@@ -651,29 +704,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     // read and a non-returning add) +3.7% / +7.4%.  (Round 4 measured the
     // counter-free insert at -2.4% before the fold and output changes.)
     if (kGwDiag && (A.diag & 8192)) {
-      int probed = 0;
-      while (probed < kTsProbeCap) {
-        const uint32_t g0 = h & ~3u;
-        const int4 kv = *reinterpret_cast<const int4*>(&s_hkey[g0]);
-        const int32_t ks[4] = {kv.x, kv.y, kv.z, kv.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if ((uint32_t)j < (h & 3u) || probed >= kTsProbeCap) continue;
-          ++probed;
-          const uint32_t sl = g0 + (uint32_t)j;
-          int32_t k = ks[j];
-          if (k == -1) {  // claim it; a lost race leaves the winner's key
-            const int32_t old = atomicCAS(&s_hkey[sl], -1, target);
-            k = old == -1 ? target : old;
-          }
-          if (k == target) {
-            atomicAdd(&s_hval[sl], val);
-            return;
-          }
-        }
-        h = g0 + 4u == (uint32_t)HASH_SLOTS ? 0u : g0 + 4u;
-      }
-      ov_add(target, val);
+      if (!cf_insert(target, val)) ov_add(target, val);
       return;
     }
     for (int probe = 0; probe < HASH_SLOTS; ++probe) {
@@ -684,7 +715,10 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       }
       if (k == -1) {
         // reserve an LDS entry first; past the load limit new keys overflow
-        if (atomicAdd(&s_hcount, 1) >= HASH_LIMIT) break;
+        // (APPEND: a full table is seen without the atomic — every
+        // overflowing key would otherwise take a returning atomic on this
+        // one LDS address)
+        if ((APPEND && s_hcount >= HASH_LIMIT) || atomicAdd(&s_hcount, 1) >= HASH_LIMIT) break;
         const int32_t old = atomicCAS(&s_hkey[h], -1, target);
         if (old == -1 || old == target) {
           atomicAdd(&s_hval[h], val);
@@ -692,6 +726,17 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         }
       }
       h = H::next(h);
+    }
+    if (APPEND && s_heavy) {  // append-and-reduce source: appended, reduced in the output phase
+      const int k = atomicAdd(&s_napp, 1);
+      if ((int64_t)k < A.app_cap) {
+        double* ab = app_base(0);
+        reinterpret_cast<int32_t*>(ab)[4 * k] = target;
+        ab[2 * k + 1] = val;
+      } else {
+        atomicOr(A.error_flag, 2);
+      }
+      return;
     }
     ov_add(target, val);
   };
@@ -870,6 +915,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         s_ncomp = 0;
         s_novc = 0;
         if (!LDS_ROW) s_ovmask = s_pm[cur].ovmask;
+        s_heavy = (APPEND && !LDS_ROW) ? s_pm[cur].heavy : 0;
+        s_napp = 0;
       }
       __syncthreads();
     } else {
@@ -1107,24 +1154,141 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         h = g0 + 4u == (uint32_t)HASH_SLOTS ? 0u : g0 + 4u;
       }
     };
+    // this thread's LDS-table slots -> the candidate list (touched / ov_list
+    // from s_novc on), cleared; keys placed by a wave scan + one LDS atomic
+    auto dump_lds = [&]() {
+      constexpr int SPT_D = HASH_SLOTS / BLOCK;
+      int32_t kk[SPT_D];
+      int mine = 0;
+#pragma unroll
+      for (int i = 0; i < SPT_D; ++i) {
+        kk[i] = s_hkey[tid + i * BLOCK];
+        mine += kk[i] != -1;
+      }
+      // (lane made opaque: its compare masks are not hoisted into scalar
+      // registers held through the whole kernel)
+      int lane = tid & 63;
+      asm volatile("" : "+v"(lane));
+      int incl = mine;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+      }
+      int wbase = 0;
+      if (lane == 63 && incl > 0) wbase = atomicAdd(&s_novc, incl);
+      int o = __shfl(wbase, 63, 64) + incl - mine;
+      const int cap34 = (int)(A.touch_cap * 3 / 4);
+#pragma unroll
+      for (int i = 0; i < SPT_D; ++i)
+        if (kk[i] != -1) {
+          const double v = s_hval[tid + i * BLOCK];
+          s_hkey[tid + i * BLOCK] = -1;
+          s_hval[tid + i * BLOCK] = 0.0;
+          if (o < cap34) {
+            __hip_atomic_store(&touched[o], kk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ov_list[o], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            atomicOr(A.error_flag, 2);
+          }
+          ++o;
+        }
+    };
+    // append-and-reduce source (PIPE, hash mode; wave 0's level build bounds its
+    // pair updates above heavy_min): the updates that found no room in the LDS
+    // table were appended (16 B each, streamed) instead of going one random
+    // CAS line each to the HBM hash.  Here: (1) appended keys that reached the
+    // LDS table anyway (the load-limit race) are folded into it, the rest
+    // counted per key-hash partition (<= 3584 entries each); (2) they are
+    // scattered into their partitions while the LDS table moves to the
+    // candidate list; (3) each partition is reduced in the emptied LDS table
+    // (counter-free insert; a key with no room within kTsProbeCap slots goes
+    // to the HBM hash, which the slot scan below compacts) and moved to the
+    // candidate list.  The selection then reads the list only.
+    const bool heavy = APPEND && !LDS_ROW && s_heavy;
+    if (heavy) {
+      int32_t* app_key = reinterpret_cast<int32_t*>(app_base(0));
+      double* app_val = app_base(0);
+      int32_t* par_key = reinterpret_cast<int32_t*>(app_base(1));
+      double* par_val = app_base(1);
+      const int napp = (int)min((int64_t)s_napp, A.app_cap);
+      int lg = 0;
+      while ((3584 << lg) < napp && lg < 6) ++lg;
+      const int NP = 1 << lg;
+      auto part = [&](int32_t key) -> int {
+        return lg ? (int)(((uint32_t)key * 0x85EBCA77u) >> (32 - lg)) : 0;
+      };
+      if (tid < 64) s_pcur[tid] = 0;
+      __syncthreads();
+      for (int k = tid; k < napp; k += BLOCK) {  // (1)
+        const int32_t key = app_key[4 * k];
+        double v = app_val[2 * k + 1];
+        fold_lds(key, v);
+        if (v == 0.0)  // folded (pair updates are > 0)
+          app_key[4 * k] = -1;
+        else
+          atomicAdd(&s_pcur[part(key)], 1);
+      }
+      __syncthreads();
+      if (tid < 64) {  // exclusive scan of the NP <= 64 partition sizes
+        int lane = tid;
+        asm volatile("" : "+v"(lane));
+        const int c = s_pcur[lane];
+        int incl = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const int y = __shfl_up(incl, d, 64);
+          if (lane >= d) incl += y;
+        }
+        s_pbase[lane] = incl - c;
+        s_pcur[lane] = incl - c;
+        if (lane == 63) s_pbase[64] = incl;
+      }
+      __syncthreads();
+      for (int k = tid; k < napp; k += BLOCK) {  // (2)
+        const int32_t key = app_key[4 * k];
+        if (key == -1) continue;
+        const int pos = atomicAdd(&s_pcur[part(key)], 1);
+        par_key[4 * pos] = key;
+        par_val[2 * pos + 1] = app_val[2 * k + 1];
+      }
+      dump_lds();
+      __syncthreads();
+      for (int p = 0; p < NP; ++p) {  // (3)
+        const int b1 = s_pbase[p + 1];
+        for (int k = s_pbase[p] + tid; k < b1; k += BLOCK) {
+          const int32_t key = par_key[4 * k];
+          const double v = par_val[2 * k + 1];
+          if (!cf_insert(key, v)) ov_add(key, v);
+        }
+        __syncthreads();
+        dump_lds();
+        __syncthreads();
+      }
+      if (tid == 0) s_hcount = 0;
+    }
     // a source with many overflow keys for its table (>= 1/8 of the slots)
     // compacts by scanning the slots in order: coalesced reads and clears
-    // instead of two random line accesses per key through `touched`
+    // instead of two random line accesses per key through `touched` (an
+    // append-and-reduce source always: its list is the candidate list)
     const uint32_t ov_mask = s_ovmask;
-    const bool ov_scan = !LDS_ROW && nov > 0 && (int64_t)s_ntouch * 8 >= (int64_t)ov_mask + 1 &&
-                         !(kGwDiag && (A.diag & 16384));  // diag bit 16384: always through `touched` (A/B)
+    const bool ov_scan = !LDS_ROW && s_ntouch > 0 &&
+                         (heavy || ((int64_t)s_ntouch * 8 >= (int64_t)ov_mask + 1 &&
+                                    !(kGwDiag && (A.diag & 16384))));  // diag bit 16384: always through `touched` (A/B)
     if (ov_scan) {
       const int T = (int)ov_mask + 1;
       const int cap34 = (int)(A.touch_cap * 3 / 4);
       const int lane = tid & 63;
       const unsigned long long below = (1ull << lane) - 1ull;
       constexpr int U = 4;
+      int ti = tid;  // (opaque: the slot addresses are formed here, not hoisted out of the source loop)
+      asm volatile("" : "+v"(ti));
       for (int b0 = 0; b0 < T; b0 += U * BLOCK) {
         int32_t key[U];
         double v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int i = b0 + u * BLOCK + tid;
+          const int i = b0 + u * BLOCK + ti;
           key[u] = -1;
           v[u] = 0.0;
           if (i < T) {
@@ -1146,7 +1310,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           if (key[u] == -1) continue;
-          const int i = b0 + u * BLOCK + tid;
+          const int i = b0 + u * BLOCK + ti;
           __hip_atomic_store(&ov_key[4 * i], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&ov_val[2 * i + 1], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           fold_lds(key[u], v[u]);
@@ -1159,6 +1323,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       }
       __syncthreads();
       nov = min(s_novc, cap34);
+    } else if (heavy) {
+      nov = min(s_novc, (int)(A.touch_cap * 3 / 4));
     } else if (!LDS_ROW && nov > 0) {
       // four entries per thread and round, their slot reads issued together
       // (the stretch compacts ~31k entries per source: the loop was a chain of
@@ -1219,7 +1385,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       // offsets: an inclusive scan inside the wave and one LDS atomic per
       // wave (the compacted order is free: selection and the sparse-row
       // writer do not depend on it); the barrier orders every read before the writes
-      const int lane = tid & 63;
+      int lane = tid & 63;
+      asm volatile("" : "+v"(lane));
       int incl = mine;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
@@ -1766,6 +1933,7 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   ws_free(t.acc_row);
   ws_free(t.ov_list);
   ws_free(t.touched);
+  ws_free(t.app);
   ws_free(t.enum_tgt);
   ws_free(t.enum_val);
   ws_free(t.dsel_id);
@@ -1827,9 +1995,12 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   t.diag_pipe = diag_pipe_max();
   const int64_t nb = pipe ? 2 : 1;
   const int64_t enum_cap = pipe ? (int64_t)step * level_cap : 1;
+  // append-and-reduce buffers (pipelined hash mode): two of app_cap 16 B
+  // entries per workgroup; a source whose pair-update bound is <= app_cap uses them
+  const int64_t app_cap = (pipe && !lds_row) ? touch_cap / 2 : 0;
   const int64_t per_block = nb * ((int64_t)(L + 1) * level_cap * 20 + spawn_cap * 20 + 4) + 2 * level_cap * 8 +
                             (level_cap + 1) * 4 + (pipe ? 2 * enum_cap * 12 : 0) +
-                            (lds_row ? 0 : touch_cap * 28) + (pipe ? TOPK_MAX * 12 : 0);
+                            (lds_row ? 0 : touch_cap * 28) + (pipe ? TOPK_MAX * 12 : 0) + app_cap * 32;
   int dev_cus = 256;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, g->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
@@ -1870,6 +2041,7 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
     GW_HIP_TRY(hipMemset(t.acc_row, 0, sizeof(double) * 2 * blocks * touch_cap));
     GW_HIP_TRY(hipMemset2D(t.acc_row, 16, 0xFF, 4, (size_t)(blocks * touch_cap)));
   }
+  if (app_cap > 0 && (rc = ws_alloc(g, &t.app, 4 * blocks * app_cap))) return rc;
   t.variant = variant;
   t.sample = sample;
   t.step = step;
@@ -1881,6 +2053,7 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   t.lds_row = mode;
   t.pipe = pipe ? 1 : 0;
   t.enum_cap = enum_cap;
+  t.app_cap = app_cap;
   t.lds_bytes = lds_row ? (size_t)n * 8 : (size_t)(mode == 2 ? TsHash<2>::SLOTS : TsHash<1>::SLOTS) * 12;
   GW_HIP_TRY(hipDeviceSynchronize());
   return GW_OK;
@@ -1942,6 +2115,9 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   A.dsel_id = t.dsel_id;
   A.dsel_val = t.dsel_val;
   A.touched = t.touched;
+  A.app = t.app;
+  A.app_cap = t.app ? t.app_cap : 0;
+  A.heavy_min = 2 * (int64_t)(t.lds_row == 1 ? TsHash<1>::LIMIT : TsHash<2>::LIMIT);
   A.src_counter = t.src_counter;
   A.error_flag = t.error_flag;
   GW_HIP_TRY(hipMemsetAsync(t.src_counter, 0, sizeof(unsigned), s));
