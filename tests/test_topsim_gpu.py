@@ -200,6 +200,48 @@ def test_topsim_stretch_pipelined_overflow(gw, oracle):
                 assert abs(sa - osc[r, k]) <= 1e-12 * osc[r, k]
 
 
+def test_topsim_stretch_many_sources_per_workgroup(gw, oracle):
+    """The stretch parameters (SAMPLE 10000 / STEP 5) on 1,536 strided sources
+    of the 1M-vertex Java R-MAT: more sources than resident workgroups, so each
+    workgroup runs several in a row, mixing append-and-reduce sources (pair-
+    update bound over 2x the LDS load limit: appended, partitioned, reduced in
+    the emptied LDS table) with light ones (LDS table, HBM hash) — the
+    append buffers, partition cursors, per-source overflow table size, LDS
+    table and HBM hash must all come back clean between sources.  Top-100 rows
+    and the exact counters against oracle.topsim_topk."""
+    import torch
+    from gwamd import _lib as Cl
+    g = gw.GWGraph.rmat_java(1_000_000, 10_000_000, 0.57, 0.19, 0.19, 42)
+    c = g.export_csr()
+    offs, nbrs = c["offsets"], c["nbrs"]
+    deg = np.diff(offs)
+    nz = np.nonzero(deg > 0)[0]
+    pick = nz[np.linspace(0, len(nz) - 1, 1536).astype(np.int64)].astype(np.int32)
+    g.to_device(0)
+    K, sample, step = 100, 10000, 5
+    src = torch.as_tensor(pick, device="cuda")
+    ids = torch.empty((len(pick), K), dtype=torch.int32, device="cuda")
+    sc = torch.empty((len(pick), K), dtype=torch.float64, device="cuda")
+    st = torch.zeros(4, dtype=torch.int64, device="cuda")
+    Cl.check(Cl.lib().gw_topsim(g.handle, 0, sample, step, 0.6, 42, Cl.ptr(src), len(pick), K, Cl.ptr(ids),
+                                Cl.ptr(sc), Cl.ptr(st), None), g.handle)
+    I, S = ids.cpu().numpy(), sc.cpu().numpy()
+    oi, osc, ost = oracle.topsim_topk(offs, nbrs, 0, sample, step, K, C=0.6, seed=42, sources=pick, nthreads=16)
+    stg = st.cpu().numpy()
+    assert int(stg[0]) == ost["extensions"] and int(stg[1]) == ost["pair_updates"]
+    assert int(stg[3]) == ost["walkers"]
+    for r in range(len(pick)):
+        m = int((oi[r] >= 0).sum())
+        got = I[r][I[r] >= 0]
+        assert len(got) == m
+        np.testing.assert_allclose(S[r, :m], osc[r, :m], rtol=1e-12)
+        omap = dict(zip(oi[r, :m].tolist(), osc[r, :m].tolist()))
+        for k, (a, b) in enumerate(zip(got.tolist(), oi[r, :m].tolist())):  # ids equal except at fp-noise ties
+            if a != b:
+                sa = omap.get(a, S[r, k])
+                assert abs(sa - osc[r, k]) <= 1e-12 * osc[r, k]
+
+
 def test_mirror_compute_and_print(gw, oracle, tmp_path):
     """TopSim_singleSample mirror + printByOrder on GPU dense rows == Java
     emulation over the oracle rows."""
