@@ -50,6 +50,7 @@ rows and no GPU work (CPU gloo test of this file); it reports no throughput.
 import argparse
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -89,6 +90,9 @@ def parse(argv):
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--allgather", choices=["auto", "on", "off"], default="auto",
                     help="time the RCCL all-gather of the walks (auto: when ranks > 1)")
+    ap.add_argument("--host-shard", choices=["auto", "on", "off"], default="auto",
+                    help="time each rank writing its own shard to pinned host memory instead of exchanging "
+                         "(SURVEY §8e's fallback; auto: when ranks > 1, and for the 1-GPU config-4 / config-5 lines)")
     ap.add_argument("--mode", choices=["auto", "bitset", "rejection"], default=None,
                     help="second-order sampler (auto: bitset when it fits in HBM)")
     ap.add_argument("--no-topsim", action="store_true")
@@ -114,6 +118,14 @@ def parse(argv):
     ap.add_argument("--topsim-sample", type=int, default=10000)
     ap.add_argument("--topsim-step", type=int, default=5)
     ap.add_argument("--topsim-graphs", default="blog", help="comma list of blog,arxiv,moreno")
+    ap.add_argument("--no-config3", action="store_true",
+                    help="skip the config-3 sweep (the reference driver's loop: blog, moreno, arxiv x SAMPLE)")
+    ap.add_argument("--config3-graphs", default="blog,moreno,arxiv")
+    ap.add_argument("--config3-samples", default="1000,2500,5000,10000,20000,40000",
+                    help="Test_u_u_TopSim_singleSample.java:36 samples (STEP 5, top-20)")
+    ap.add_argument("--config3-cpu-samples", default="1000,10000,40000",
+                    help="sweep points that also time the CPU oracle")
+    ap.add_argument("--config3-cpu-seconds", type=float, default=3.0)
     ap.add_argument("--p10m-vertices", type=int, default=10_000_000,
                     help="config 5 graph size (BASELINE: 10M vertices, 10 R-MAT lines per vertex); smaller for tests")
     ap.add_argument("--plumbing-check", action="store_true",
@@ -430,6 +442,76 @@ def gather_timing(R, args, step, out, L, B, begin_of=None, count_of=None):
             "check_last_rank_block_identical": check}, ok
 
 
+HOST_PIN_LIMIT = 16 << 30  # a rank's host shard is pinned up to this size, else pageable
+
+
+def host_buffer(R, shape, dtype):
+    """Host memory for a rank's shard: pinned (page-locked, DMA target) up to
+    HOST_PIN_LIMIT bytes, pageable above it and in CPU rehearsals."""
+    torch = R.torch
+    nbytes = dtype.itemsize if hasattr(dtype, "itemsize") else torch.empty((), dtype=dtype).element_size()
+    for d in shape:
+        nbytes *= d
+    pin = R.dev.type == "cuda" and nbytes <= HOST_PIN_LIMIT
+    return torch.empty(shape, dtype=dtype, pin_memory=pin), pin
+
+
+def walk_host_shard_timing(R, args, steps, write, recompute, host, first, cnt, pinned, units):
+    """SURVEY §8e's alternative to the all-gather: every rank writes its own
+    walk shard straight to host memory (the reference's multi-worker split
+    writes per-worker files, SingleRandomWalkApproxMultiThreads.java:59, 174)
+    — no collective.  `write(i)` walks step i's shard into `host`
+    (gw_n2v_walks_host: chunks walked on one stream while the previous chunk is
+    copied out on another).  Timed like the headline (barrier + max over
+    ranks); each rank then checks three row windows of its host shard of the
+    last step against a device recomputation of the same walks."""
+    torch = R.torch
+    el, _ = time_steps(R, lambda i, ev: write(i), steps, 0, events=False)
+    last = steps - 1
+    ok = True
+    for lo in sorted({0, max(0, cnt // 2 - 500), max(0, cnt - 1000)}):
+        n = min(1000, cnt - lo)
+        if n <= 0:
+            continue
+        mine = recompute(first(last) + lo, n).cpu()
+        ok = ok and bool(torch.equal(host[lo:lo + n], mine))
+    allok = R.allreduce([0.0 if ok else 1.0], "max")[0] == 0.0
+    nbytes = cnt * host.shape[1] * 4
+    return {"seconds": el, "ms_per_step": el / steps * 1e3, "value": units / el,
+            "unit": "walk-steps/s (each rank's walks written to its host memory)",
+            "bytes_per_step_per_rank": nbytes, "host_GBps_per_rank": nbytes * steps / el / 1e9,
+            "host_memory": "pinned" if pinned else "pageable",
+            "mode": "gw_n2v_walks_host: walk chunk k+1 while chunk k is copied D2H (no collective)",
+            "check_host_rows_equal_device_rows": bool(allok)}
+
+
+def topk_host_shard_timing(R, args, run, ids, sc, nloc, upd):
+    """TopSim + each rank's own top-k rows copied to host memory (no
+    exchange), beside the all-gather; also the copy alone."""
+    torch = R.torch
+    K = ids.shape[1]
+    hid, pinned = host_buffer(R, (max(nloc, 1), K), torch.int32)
+    hsc, _ = host_buffer(R, (max(nloc, 1), K), torch.float64)
+
+    def copy():
+        hid[:nloc].copy_(ids[:nloc], non_blocking=True)
+        hsc[:nloc].copy_(sc[:nloc], non_blocking=True)
+
+    def both(i, ev):
+        run(None)
+        copy()
+    el, _ = time_steps(R, both, 1, 0, events=False)
+    cel, _ = time_steps(R, lambda i, ev: copy(), 1, 0, events=False)
+    ok = bool(torch.equal(hid[:nloc], ids[:nloc].cpu()) and torch.equal(hsc[:nloc], sc[:nloc].cpu()))
+    allok = R.allreduce([0.0 if ok else 1.0], "max")[0] == 0.0
+    nbytes = nloc * K * 12
+    return {"seconds": el, "value": upd / el if upd else None,
+            "unit": "pair-updates/s (each rank's top-k rows copied to its host memory)",
+            "d2h_only_s": cel, "bytes_per_rank": nbytes, "host_GBps_per_rank": nbytes / max(cel, 1e-9) / 1e9,
+            "host_memory": "pinned" if pinned else "pageable", "mode": "TopSim, then its rows D2H (no collective)",
+            "check_host_rows_equal_device_rows": bool(allok)}
+
+
 def checksum(t):
     """Position-weighted checksum of a tensor's bytes (int64, device-side)."""
     import torch
@@ -526,6 +608,14 @@ def walk_headline(R, args):
             g, ok = gather_timing(R, args, step, out, L, B, begin_of, count_of)
             res["allgather"] = g
             res["allgather_all_ranks_ok"] = bool(ok[0] >= 1.0)
+        if args.host_shard == "on" or (args.host_shard == "auto" and world > 1):
+            host, pinned = host_buffer(R, (cnt_w, L), torch.int32)
+
+            def write(i):
+                step(i, None)
+                host.copy_(out[:cnt_w])
+            res["host_shard"] = walk_host_shard_timing(R, args, args.steps, write, synth, host, first, cnt_w, pinned,
+                                                       steps_total)
         return res
 
     import gwamd
@@ -649,6 +739,8 @@ def walk_headline(R, args):
         g["xgmi_GBps_per_rank"] = g["gathered_bytes_per_step_per_rank"] * args.steps / g["seconds"] / 1e9
         res["allgather"] = g
         res["allgather_all_ranks_ok"] = bool(ok[0] >= 1.0)
+    if args.host_shard == "on" or (args.host_shard == "auto" and world > 1):
+        res["host_shard"] = walks_to_host(R, args, G, L, first, cnt_w, args.steps, recompute, steps_total)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_walks(G.export_csr(), args.p, args.q, args.seed, L, 0, args.cpu_seconds)
     if rank == 0:
@@ -684,6 +776,20 @@ def walk_headline(R, args):
     del out
     G.free()
     return res
+
+
+def walks_to_host(R, args, G, L, first, cnt, steps, recompute, units):
+    """This rank's walks of `steps` steps written to host memory by
+    gw_n2v_walks_host (see walk_host_shard_timing)."""
+    torch = R.torch
+    from gwamd import _lib as C
+    host, pinned = host_buffer(R, (cnt, L), torch.int32)
+
+    def write(i):
+        C.check(C.lib().gw_n2v_walks_host(G.handle, L, args.seed, first(i), cnt, 1, C.ptr(host), None, None),
+                G.handle)
+    write(0)  # first touch of the host pages, device staging buffers
+    return walk_host_shard_timing(R, args, steps, write, recompute, host, first, cnt, pinned, units)
 
 
 def walk_roofline(kname, tag, steps, kernel_s, table_bytes, grid):
@@ -810,6 +916,9 @@ def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejectio
         g["xgmi_GBps_per_rank"] = g["gathered_bytes_per_step_per_rank"] / g["seconds"] / 1e9
         g["all_ranks_ok"] = bool(ok[0] >= 1.0)
         gather = g
+    host = None
+    if strong_walks and (args.host_shard == "on" or (args.host_shard == "auto")):
+        host = walks_to_host(R, args, BG, L, lambda i: first(1 + i), nb, 1, recompute, bsteps)
     cpu_b = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu_b = cpu_baseline_walks(BG.export_csr(), wp, wq, args.seed, L, 0, 10.0, max_walks=2_000_000)
@@ -875,7 +984,7 @@ def walk_secondary(R, args, BG, build_s, wp, wq, scale, ef, what, force_rejectio
                          "random_line_roofline": line},
             "host_build_s": build_s, "prepare_s": bprep, "sampler_tables_gb": sbytes / 1e9,
             "end_to_end": e2e, "end_to_end_rejection": e2e_rej, "end_to_end_best": e2e_best,
-            "allgather": gather, "cpu_baseline": cpu_b}
+            "allgather": gather, "host_shard": host, "cpu_baseline": cpu_b}
 
 
 TOPSIM_GRAPHS = {"blog": ("blog.txt", 10313, ",", "lshrank blog, V=10313, 333,983 edges"),
@@ -883,7 +992,32 @@ TOPSIM_GRAPHS = {"blog": ("blog.txt", 10313, ",", "lshrank blog, V=10313, 333,98
                  "moreno": ("moreno_crime_crime.txt", 1380, "\t", "lshrank moreno, V=1380, 1,476 edges")}
 
 
-def topsim_roofline(ext, upd, kt, tag, nsrc, nnz, step, n=None):
+_TS_DISPATCH = {}  # kernel name -> gw_topsim* dispatches of it so far in this process
+
+
+def ts_dispatch(h, call):
+    """Run one gw_topsim* call; return (the kernel it dispatched, the ordinal
+    of that dispatch among this process's dispatches of the same kernel).  The
+    PMC passes run the same bench command, so tools/pmc_summary.py picks the
+    timed dispatch of a line by that ordinal (lines that share a kernel — the
+    config-3 sweep — are told apart by it, not by name or grid)."""
+    from gwamd import _lib as C
+    call()
+    name = C.lib().gw_topsim_kernel(h).decode()
+    k = _TS_DISPATCH.get(name, 0)
+    _TS_DISPATCH[name] = k + 1
+    return name, k
+
+
+def ts_kernel_attrs(h):
+    """VGPRs and scratch per lane, LDS per workgroup of the handle's TopSim kernel."""
+    from gwamd import _lib as C
+    v, sc, lds = C.ctypes.c_int32(), C.ctypes.c_int32(), C.ctypes.c_int32()
+    C.check(C.lib().gw_topsim_kernel_attrs(h, C.ctypes.byref(v), C.ctypes.byref(sc), C.ctypes.byref(lds)), h)
+    return {"vgprs": v.value, "scratch_bytes_per_lane": sc.value, "lds_bytes_per_workgroup": lds.value}
+
+
+def topsim_roofline(ext, upd, kt, tag, nsrc, nnz, step, n=None, kernel=None, nth=None):
     """52 B per path extension + 24 B per pair-update / kernel time.
     The denominator follows where the data lives: the slot table (16 B per
     adjacency entry) and the level records of lshrank graphs stay in the 256 MB
@@ -904,11 +1038,13 @@ def topsim_roofline(ext, upd, kt, tag, nsrc, nnz, step, n=None):
     return {"bound": bound, "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
             "traffic": prof["hbm_bytes_per_launch"] if prof else None,
             "traffic_GBps": prof["hbm_bytes_per_launch"] / kt / 1e9 if prof else None,
-            "algorithmic_bytes": alg, "slot_table_bytes": table, "kernel": "k_topsim", "kernel_ms": kt * 1e3,
-            "units_per_launch": nsrc, "pmc_tag": tag,
-            # dense-row (lshrank) and hash-mode (P10M) kernels are told apart by name, STEP by the template argument
-            "pmc_match": {"kernel": (f"k_topsim(_pipe_row)?<{step}[,>]" if n is not None and n * 8 <= 96 * 1024
-                                     else f"k_topsim(_2wg|_pipe)<{step}[,>]"), "grid": None},
+            "algorithmic_bytes": alg, "slot_table_bytes": table, "kernel": kernel or "k_topsim",
+            "kernel_ms": kt * 1e3, "units_per_launch": nsrc, "pmc_tag": tag,
+            # the timed dispatch: the exact kernel and its ordinal among this process's dispatches of it
+            "pmc_match": ({"kernel": "^" + re.escape(kernel) + "$", "grid": None, "nth": [nth]} if kernel else
+                          {"kernel": (f"k_topsim(_pipe_row)?<{step}[,>]" if n is not None and n * 8 <= 96 * 1024
+                                      else f"k_topsim(_2wg|_pipe)<{step}[,>]"), "grid": None}),
+            "scratch_bytes_per_lane": prof.get("scratch_bytes") if prof else None,
             "random_line_roofline": line_roofline(prof, kt, table, 128)}
 
 
@@ -931,10 +1067,14 @@ def p10m_graph(R, args):
     return _P10M_GRAPH[key]
 
 
-def run_topsim(R, args, name, p10m_sample=None, p10m_step=None, stride=1):
-    """TopSim_singleSample: lshrank graphs (config 3; every rank all sources) or
-    P10M (config 5 at SAMPLE 1000 / STEP 3, or the SURVEY §8d stretch
-    SAMPLE 10000 / STEP 5; sources split over ranks, strong scaling)."""
+def run_topsim(R, args, name, sample=None, step=None, stride=1, cpu_seconds=None, cpu=True):
+    """TopSim_singleSample: lshrank graphs (config 3; every rank all sources;
+    default SAMPLE / STEP from --topsim-sample / --topsim-step) or P10M
+    (config 5 at SAMPLE 1000 / STEP 3, or the SURVEY §8d stretch SAMPLE 10000
+    / STEP 5; sources split over ranks, strong scaling).  At ranks > 1 the P10M
+    rows are all-gathered (RCCL) and, beside it, every rank's own rows are
+    copied to pinned host memory (SURVEY §8e's per-rank output, the reference's
+    per-worker files: SingleRandomWalkApproxMultiThreads.java:59, 174)."""
     import numpy as np
     torch = R.torch
     import gwamd
@@ -942,7 +1082,9 @@ def run_topsim(R, args, name, p10m_sample=None, p10m_step=None, stride=1):
     from gwamd import dist as gdist
     from gwamd import topsim
     world, rank = R.world, R.rank
-    K, sample, step = 20, args.topsim_sample, args.topsim_step
+    K = 20
+    if name != "p10m":
+        sample, step = sample or args.topsim_sample, step or args.topsim_step
     offs = nbrs = None
     if R.plumbing:  # config 5's rank / collective path with synthetic rows (no GPU)
         K, nsrc_all = 100, 1 << args.scale
@@ -957,10 +1099,14 @@ def run_topsim(R, args, name, p10m_sample=None, p10m_step=None, stride=1):
             sc[:len(srcs)] = s_.to(torch.float64) + torch.arange(K, dtype=torch.float64) / K
         synth()
         g = gather_rows_timing(R, args, [ids, sc], run=synth) if world > 1 else None
+        host = None
+        if args.host_shard == "on" or (args.host_shard == "auto" and world > 1):
+            host = topk_host_shard_timing(R, args, lambda _: synth(), ids, sc, len(srcs), 0)
         return {"metric": "SimRank pair-updates/sec (TopSim_singleSample)", "value": None, "unit": "pair-updates/s",
                 "n_ranks": world, "scaling": "strong", "seconds": g["seconds"] if g else 0.0,
                 "config": {"workload": f"plumbing: {nsrc_all} synthetic top-{K} rows split round-robin",
-                           "topk": K}, "pair_updates": 0, "cpu_baseline": None, "roofline": None, "allgather": g}
+                           "topk": K}, "pair_updates": 0, "cpu_baseline": None, "roofline": None, "allgather": g,
+                "host_shard": host}
     if name == "p10m":
         # config 5: 10M-vertex Java-semantics R-MAT (reference quadrant recursion),
         # 1e8 generated lines, all non-isolated sources, top-100
@@ -975,7 +1121,7 @@ def run_topsim(R, args, name, p10m_sample=None, p10m_step=None, stride=1):
         srcs = srcs_all[rank::world]
         desc = (f"{args.p10m_vertices} vertices, {10 * args.p10m_vertices} R-MAT lines, {len(srcs_all)} non-isolated "
                 f"sources" + (f" (every {stride}th)" if stride > 1 else "") + f" split round-robin over {world} rank(s)")
-        K, sample, step = 100, p10m_sample or 1000, p10m_step or 3
+        K, sample, step = 100, sample or 1000, step or 3
         scaling = "strong"
         keep = pg
     else:
@@ -996,9 +1142,14 @@ def run_topsim(R, args, name, p10m_sample=None, p10m_step=None, stride=1):
     stream = torch.cuda.current_stream(R.dev)
     sh = C.ctypes.c_void_p(stream.cuda_stream)
 
+    last = {}
+
     def ts_run(stats_ptr):
-        C.check(C.lib().gw_topsim(h, C.TOPSIM_SINGLE_SAMPLE, sample, step, 0.6, args.seed, C.ptr(src), nloc, K,
-                                  C.ptr(ids), C.ptr(sc), stats_ptr, sh), h)
+        if nloc == 0:
+            return
+        last["kernel"], last["nth"] = ts_dispatch(h, lambda: C.check(
+            C.lib().gw_topsim(h, C.TOPSIM_SINGLE_SAMPLE, sample, step, 0.6, args.seed, C.ptr(src), nloc, K,
+                              C.ptr(ids), C.ptr(sc), stats_ptr, sh), h))
 
     ts_run(None)  # warm-up (also sizes the workspace)
     torch.cuda.synchronize()
@@ -1010,6 +1161,8 @@ def run_topsim(R, args, name, p10m_sample=None, p10m_step=None, stride=1):
         if ev is not None:
             ev[1].record(stream)
     tel, kms = time_steps(R, tstep, 1, 0)
+    timed = dict(last)
+    kattrs = ts_kernel_attrs(h) if nloc else None
     ext_l, upd_l = int(st[0].item()), int(st[1].item())
     ext, upd = (int(x) for x in R.allreduce([ext_l, upd_l], "sum", torch.int64))
     gather = None
@@ -1034,11 +1187,15 @@ def run_topsim(R, args, name, p10m_sample=None, p10m_step=None, stride=1):
                       value=upd / gboth["seconds"], unit="pair-updates/s (top-k rows all-gathered to every rank)",
                       check_blocks_match_sender_checksums=gonly["check_blocks_match_sender_checksums"] and
                       gboth["check_blocks_match_sender_checksums"])
+    host = None
+    if name == "p10m" and stride == 1 and args.host_shard != "off":
+        host = topk_host_shard_timing(R, args, ts_run, ids, sc, nloc, upd)
     tag = f"topsim_{name}_s{sample}_t{step}_k{K}" + (f"_stride{stride}" if stride > 1 else "")
     cpu_ts = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu:
         cpu_ts = cpu_baseline_topsim(offs, nbrs, len(offs) - 1, sample, step, args.seed,
-                                     args.cpu_seconds if name != "p10m" else 15.0, sources=srcs, topk=K)
+                                     cpu_seconds or (args.cpu_seconds if name != "p10m" else 15.0), sources=srcs,
+                                     topk=K)
     if name == "p10m":
         desc += f", SAMPLE {sample}, STEP {step}" + (" (SURVEY §8d stretch)" if (sample, step) != (1000, 3) else "")
     del keep
@@ -1048,8 +1205,36 @@ def run_topsim(R, args, name, p10m_sample=None, p10m_step=None, stride=1):
         "config": {"workload": f"TopSim_singleSample on {name} ({desc}, Java multigraph)",
                    "step": step, "sample": sample, "C": 0.6, "topk": K},
         "pair_updates": upd, "path_extensions": ext, "seconds": tel, "cpu_baseline": cpu_ts, "allgather": gather,
-        "roofline": topsim_roofline(ext_l, upd_l, kms * 1e-3, tag, nloc, int(offs[-1]), step, len(offs) - 1),
+        "host_shard": host, "kernel": timed.get("kernel"), "kernel_attrs": kattrs,
+        "roofline": topsim_roofline(ext_l, upd_l, kms * 1e-3, tag, nloc, int(offs[-1]), step, len(offs) - 1,
+                                    timed.get("kernel"), timed.get("nth")),
     }
+
+
+def run_config3_sweep(R, args):
+    """BASELINE config 3 as the reference driver runs it
+    (Test_u_u_TopSim_singleSample.java:28-42, MyConfiguration.java:27-32):
+    TopSim_singleSample on lshrank blog, moreno and arxiv (the driver's files
+    0-2; file 3, power_biGraph_10000_5, is not in the reference) at STEP 5 for
+    every SAMPLE of its loop, all sources, top-20 rows (testTopK = {20}).
+    Each point: the kernel dispatched and its registers / scratch, the roofline
+    with the keyed PMC traffic of that dispatch, and (at --config3-cpu-samples)
+    the CPU oracle on a bounded strided sample."""
+    cpu_at = {int(x) for x in args.config3_cpu_samples.split(",") if x}
+    pts = []
+    for name in args.config3_graphs.split(","):
+        for sample in (int(x) for x in args.config3_samples.split(",")):
+            pts.append(run_topsim(R, args, name, sample, 5, cpu_seconds=args.config3_cpu_seconds,
+                                  cpu=sample in cpu_at))
+            p = pts[-1]
+            log(f"[config 3] {name} SAMPLE {sample}: {p['value']:.3e} pair-updates/s, {p['seconds'] * 1e3:.2f} ms, "
+                f"{p['kernel']} {p['kernel_attrs']}")
+    return {"metric": "SimRank pair-updates/sec (TopSim_singleSample, the reference driver's sweep)",
+            "unit": "pair-updates/s",
+            "config": {"workload": "Test_u_u_TopSim_singleSample loop: lshrank blog / moreno / arxiv, STEP 5, "
+                                   f"SAMPLE in {args.config3_samples}, every source, top-20"},
+            "points": [{"graph": p["config"]["workload"].split(" ")[2], "sample": p["config"]["sample"], **p}
+                       for p in pts]}
 
 
 LDS_CALIB_FILE = os.path.join(ROOT, "profiles", "r03", "calib_lds.jsonl")
@@ -1198,8 +1383,13 @@ def main(argv):
     sec_mode = args.secondary
     if not R.plumbing and sec_mode != "none" and args.config == 2:
         if R.world == 1 or sec_mode == "all":
+            if not args.no_config3:
+                secondary["topsim_config3"] = run_config3_sweep(R, args)
             if not args.no_topsim:
-                res = [run_topsim(R, args, nm) for nm in args.topsim_graphs.split(",")]
+                done = {(p["graph"], p["sample"], p["config"]["step"]): p
+                        for p in (secondary.get("topsim_config3") or {}).get("points", [])}
+                res = [done.get((nm, args.topsim_sample, args.topsim_step)) or run_topsim(R, args, nm)
+                       for nm in args.topsim_graphs.split(",")]
                 secondary["topsim"] = res[0]
                 if len(res) > 1:
                     secondary["topsim"]["more"] = res[1:]
@@ -1263,6 +1453,8 @@ def main(argv):
             res["pair_updates"] = head["pair_updates"]
             if head.get("allgather"):
                 res["allgather"] = head["allgather"]
+            if head.get("host_shard"):
+                res["host_shard"] = head["host_shard"]
         else:
             a, b, c = rmat_abc(args)
             res["config"] = {
@@ -1288,6 +1480,8 @@ def main(argv):
             if "allgather" in head:
                 res["allgather"] = head["allgather"]
                 res["allgather_all_ranks_ok"] = head["allgather_all_ranks_ok"]
+            if "host_shard" in head:
+                res["host_shard"] = head["host_shard"]
         ref = reference_cpu_fixture()
         if ref and not R.plumbing:
             res["reference_cpu_context"] = {"file": "profiles/cpu_reference_node2vec.json",

@@ -130,6 +130,7 @@ struct gw_topsim_ws {
   double* dsel_val = nullptr;
   unsigned int* src_counter = nullptr;  // work queue head
   int* error_flag = nullptr;      // capacity overflow
+  char kernel[32] = {0};          // the kernel this workspace launches (gw_topsim_kernel)
 };
 
 // TopSim sparse rows (gw_topsim_sparse): per source r, row_len[r] nonzero

@@ -494,11 +494,16 @@ __device__ __forceinline__ TsLevelStats ts_wave_levels(const TsArgs& A, int b, i
       // the source's overflow hash (hash mode): pair updates it can make are
       // STEP per walker + the enumerated ones, so no more distinct overflow
       // keys; the power of two above 9/8 of that bound (<= touch_cap)
-      const int64_t ub = abort ? 0 : min((int64_t)G.n, (int64_t)nwk * STEP + min(nct, (int)A.enum_cap));
+      // Distinct keys are also <= n, but appended pair updates repeat keys:
+      // the append-and-reduce choice uses the uncapped pair-update bound
+      // (a small graph at a large SAMPLE can make more updates than app_cap
+      // holds while n <= app_cap; such a source keeps the HBM hash)
+      const int64_t pairs = abort ? 0 : (int64_t)nwk * STEP + min(nct, (int)A.enum_cap);
+      const int64_t ub = min((int64_t)G.n, pairs);
       int64_t t = 64;
       while (t < ub + ub / 8 + 1 && t < A.touch_cap) t <<= 1;
       s_pm[b].ovmask = (uint32_t)(t - 1);
-      s_pm[b].heavy = A.app_cap > 0 && ub > A.heavy_min && ub <= A.app_cap && !(kGwDiag && (A.diag & (32768 | 8192)));
+      s_pm[b].heavy = A.app_cap > 0 && pairs > A.heavy_min && pairs <= A.app_cap && !(kGwDiag && (A.diag & (32768 | 8192)));
       s_pm[b].valid = 1;
     }
   }
@@ -1318,6 +1323,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           if (k < cap34) {
             __hip_atomic_store(&touched[k], key[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&ov_list[k], v[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            atomicOr(A.error_flag, 2);  // as dump_lds / ov_add at the same limit
           }
         }
       }
@@ -1834,6 +1841,30 @@ hipError_t launch_mode(int mode, bool pipe, const TsArgs& A, int blocks, size_t 
   return lds <= TS_2WG_LDS ? launch_step<STEP, 0, true>(A, blocks, lds, s) : launch_step<STEP, 0, false>(A, blocks, lds, s);
 }
 
+// the kernel launch_mode() dispatches (gw_topsim_kernel_attrs)
+template <int STEP>
+const void* kernel_fn(int mode, bool pipe, size_t lds) {
+  if (mode == 2 && pipe) return (const void*)k_topsim_pipe<STEP>;
+  if (mode == 0 && pipe) return (const void*)k_topsim_pipe_row<STEP>;
+  if (mode == 2) return (const void*)k_topsim_2wg<STEP, 2>;
+  if (mode == 1) return (const void*)k_topsim<STEP, 1>;
+  return lds <= TS_2WG_LDS ? (const void*)k_topsim_2wg<STEP, 0> : (const void*)k_topsim<STEP, 0>;
+}
+
+const void* kernel_fn(int step, int mode, bool pipe, size_t lds) {
+  switch (step) {
+    case 1: return kernel_fn<1>(mode, pipe, lds);
+    case 2: return kernel_fn<2>(mode, pipe, lds);
+    case 3: return kernel_fn<3>(mode, pipe, lds);
+    case 4: return kernel_fn<4>(mode, pipe, lds);
+    case 5: return kernel_fn<5>(mode, pipe, lds);
+    case 6: return kernel_fn<6>(mode, pipe, lds);
+    case 7: return kernel_fn<7>(mode, pipe, lds);
+    case 8: return kernel_fn<8>(mode, pipe, lds);
+    default: return nullptr;
+  }
+}
+
 hipError_t launch(int step, int mode, bool pipe, const TsArgs& A, int blocks, size_t lds, hipStream_t s) {
   switch (step) {
     case 1: return launch_mode<1>(mode, pipe, A, blocks, lds, s);
@@ -2055,6 +2086,15 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   t.enum_cap = enum_cap;
   t.app_cap = app_cap;
   t.lds_bytes = lds_row ? (size_t)n * 8 : (size_t)(mode == 2 ? TsHash<2>::SLOTS : TsHash<1>::SLOTS) * 12;
+  // the kernel launch() dispatches for this workspace (gw_topsim_kernel)
+  if (mode == 2 && pipe)
+    std::snprintf(t.kernel, sizeof t.kernel, "k_topsim_pipe<%d>", step);
+  else if (mode == 0 && pipe)
+    std::snprintf(t.kernel, sizeof t.kernel, "k_topsim_pipe_row<%d>", step);
+  else if (mode == 2 || (mode == 0 && t.lds_bytes <= TS_2WG_LDS))
+    std::snprintf(t.kernel, sizeof t.kernel, "k_topsim_2wg<%d, %d>", step, mode);
+  else
+    std::snprintf(t.kernel, sizeof t.kernel, "k_topsim<%d, %d>", step, mode);
   GW_HIP_TRY(hipDeviceSynchronize());
   return GW_OK;
 }
@@ -2155,6 +2195,26 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
     g->err = "sparse rows exceed the output capacity (rows with len -1 did not fit; *used = room needed)";
     return GW_ERR_CAPACITY;
   }
+  return GW_OK;
+}
+
+extern "C" const char* gw_topsim_kernel(const gw_graph* g) {
+  return g ? g->ts.kernel : "";
+}
+
+extern "C" int gw_topsim_kernel_attrs(gw_graph* g, int32_t* vgprs, int32_t* scratch_bytes, int32_t* lds_bytes) {
+  if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
+  const gw_topsim_ws& t = g->ts;
+  if (t.blocks == 0) return gw_fail(g, GW_ERR_STATE, "no TopSim workspace (call gw_topsim_prepare)");
+  GW_GUARD_DEVICE(g, g->device);
+  const void* fn = kernel_fn(t.step, t.lds_row, t.pipe != 0, t.lds_bytes);
+  if (!fn) return gw_fail(g, GW_ERR_STATE, "no TopSim kernel for step %d", t.step);
+  hipFuncAttributes fa;
+  const hipError_t e = hipFuncGetAttributes(&fa, fn);
+  if (e != hipSuccess) return gw_fail(g, GW_ERR_DEVICE, "hipFuncGetAttributes: %s", hipGetErrorString(e));
+  if (vgprs) *vgprs = (int32_t)fa.numRegs;
+  if (scratch_bytes) *scratch_bytes = (int32_t)fa.localSizeBytes;
+  if (lds_bytes) *lds_bytes = (int32_t)(fa.sharedSizeBytes + t.lds_bytes);
   return GW_OK;
 }
 

@@ -121,6 +121,8 @@ SIGNATURES = {
     "gw_topsim_host": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, U64, P, I64,
                                       ctypes.c_int, P, P, P, P]),
     "gw_topsim_prepare":(ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "gw_topsim_kernel": (ctypes.c_char_p, [P]),
+    "gw_topsim_kernel_attrs": (ctypes.c_int, [P, P, P, P]),
     "gw_topsim": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, U64, P, I64,
                                  ctypes.c_int, P, P, P, P]),
     "gw_topsim_dense": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, U64, P, I64,

@@ -268,6 +268,14 @@ int gw_n2v_walks_host(gw_graph* g, int walk_len, uint64_t seed,
 /* Allocate the per-workgroup workspace for up to `sample`/`step` (kept in the
  * handle; sizes the level arrays and the accumulator rows).                 */
 int gw_topsim_prepare(gw_graph* g, int variant, int sample, int step, int topk);
+/* Name of the kernel the handle's prepared TopSim workspace launches (e.g.
+ * "k_topsim_pipe<5>", "k_topsim_2wg<5, 2>", "k_topsim_pipe_row<5>"; "" before
+ * the first gw_topsim_prepare / gw_topsim* call).  Diagnostic: the choice
+ * depends on V, SAMPLE and STEP (no reference counterpart).                 */
+const char* gw_topsim_kernel(const gw_graph* g);
+/* Registers per lane, private segment (scratch) bytes per lane and LDS bytes
+ * per workgroup (static + dynamic) of that kernel (hipFuncGetAttributes).   */
+int gw_topsim_kernel_attrs(gw_graph* g, int32_t* vgprs, int32_t* scratch_bytes, int32_t* lds_bytes);
 /* Replaces new TopSim_singleSample(g, sample, step).compute() +
  * Print.printByOrder's per-row FixedMaxPQ (TopSim_singleSample.java:35-54,
  * Print.java:25-53) for the given sources: out_ids_dev[nsrc*topk],

@@ -46,6 +46,9 @@ def test_bench_two_ranks_gloo_on_gpu():
     assert res["walk_steps"] == 2 * 2 * 10 * n * 79
     assert res["allgather"]["check_last_rank_block_identical"] is True
     assert res["allgather_all_ranks_ok"] is True
+    h = res["host_shard"]  # gw_n2v_walks_host into pinned memory, rows equal the device walks
+    assert h["check_host_rows_equal_device_rows"] is True and h["host_memory"] == "pinned"
+    assert h["bytes_per_step_per_rank"] == 10 * n * 80 * 4
 
 
 @pytest.mark.gpu
@@ -69,6 +72,8 @@ def test_bench_config4_strong_two_ranks_gloo_on_gpu():
     assert res["walk_steps"] <= 2 * total * 79 and res["walk_steps"] > 0
     assert res["allgather"]["check_last_rank_block_identical"] is True and res["allgather_all_ranks_ok"] is True
     assert res["end_to_end"]["prepare_s"] >= 0 and res["end_to_end"]["value"] > 0
+    h = res["host_shard"]
+    assert h["check_host_rows_equal_device_rows"] is True and h["value"] > 0
 
 
 @pytest.mark.gpu
@@ -81,3 +86,33 @@ def test_bench_config5_two_ranks_rows_allgather_gloo_on_gpu():
     assert rc == 0, err[-3000:]
     assert res["scaling"] == "strong" and res["ranks"] == 2 and res["value"] > 0
     assert res["allgather"]["check_blocks_match_sender_checksums"] is True
+    h = res["host_shard"]
+    assert h["check_host_rows_equal_device_rows"] is True and h["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_config3_sweep_small():
+    """The config-3 sweep (Test_u_u_TopSim_singleSample's loop) at two SAMPLEs on
+    moreno and arxiv: one point per (graph, SAMPLE), each naming the kernel it
+    dispatched with its registers / scratch, the timed dispatch's ordinal for
+    the PMC passes, and a CPU oracle baseline where asked."""
+    rc, res, err = _run(["--scale", "10", "--steps", "1", "--warmup", "0", "--no-walk10m", "--no-simrank",
+                         "--no-rmat24", "--no-p10m", "--no-p10m-stretch", "--no-arxiv", "--topsim-graphs", "moreno",
+                         "--config3-graphs", "moreno,arxiv", "--config3-samples", "1000,5000",
+                         "--config3-cpu-samples", "1000", "--config3-cpu-seconds", "0.5", "--cpu-seconds", "0.5"])
+    assert rc == 0, err[-3000:]
+    sw = res["secondary"]["topsim_config3"]
+    pts = sw["points"]
+    assert [(p["graph"], p["sample"]) for p in pts] == [("moreno", 1000), ("moreno", 5000), ("arxiv", 1000),
+                                                        ("arxiv", 5000)]
+    for p in pts:
+        assert p["value"] > 0 and p["kernel"].startswith("k_topsim") and p["config"]["step"] == 5
+        assert p["kernel_attrs"]["vgprs"] > 0 and p["kernel_attrs"]["scratch_bytes_per_lane"] >= 0
+        m = p["roofline"]["pmc_match"]
+        assert m["nth"][0] >= 0 and p["kernel"] in m["kernel"]
+        assert (p["cpu_baseline"] is not None) == (p["sample"] == 1000)
+    assert pts[0]["kernel"] == "k_topsim_2wg<5, 0>"  # moreno: the dense LDS row at two workgroups per CU
+    assert pts[2]["kernel"] == "k_topsim_pipe<5>"    # arxiv, SAMPLE <= 2048: the pipelined hash kernel
+    assert pts[3]["kernel"] == "k_topsim_2wg<5, 2>"  # arxiv 5000: W/E < 16 keeps the unpipelined kernel
+    # the moreno line of secondary.topsim is NOT a second run of the sweep's point at another SAMPLE
+    assert res["secondary"]["topsim"]["config"]["sample"] == 10000

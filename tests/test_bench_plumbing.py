@@ -47,6 +47,10 @@ def test_bench_multi_rank_plumbing(ranks, limit):
         assert g["mode"] == f"ring of {limit // (ranks * L * 4)}-row chunks"
     else:
         assert g["mode"] == "whole"
+    # SURVEY §8e's alternative exchange: every rank writes its own shard to host memory
+    h = res["host_shard"]
+    assert h["check_host_rows_equal_device_rows"] is True
+    assert h["bytes_per_step_per_rank"] == B * L * 4 and h["seconds"] > 0
 
 
 @pytest.mark.parametrize("ranks", [2, 4])
@@ -68,6 +72,9 @@ def test_bench_config4_strong_plumbing(ranks):
     assert g["check_last_rank_block_identical"] is True and res["allgather_all_ranks_ok"] is True
     rows = -(-total // ranks)
     assert g["gathered_bytes_per_step_per_rank"] == (ranks - 1) * rows * L * 4
+    h = res["host_shard"]  # the shard written to host memory instead of gathered
+    assert h["check_host_rows_equal_device_rows"] is True
+    assert total // ranks * L * 4 <= h["bytes_per_step_per_rank"] <= rows * L * 4
 
 
 @pytest.mark.parametrize("ranks", [2, 4])
@@ -84,6 +91,9 @@ def test_bench_config5_rows_allgather_plumbing(ranks):
     assert g["check_blocks_match_sender_checksums"] is True
     rows = -(-(1 << scale) // ranks)
     assert g["gathered_bytes_per_step_per_rank"] == (ranks - 1) * rows * K * 12
+    h = res["host_shard"]  # each rank's own rows to host memory, no exchange
+    assert h["check_host_rows_equal_device_rows"] is True
+    assert (1 << scale) // ranks * K * 12 <= h["bytes_per_rank"] <= rows * K * 12
 
 
 def test_bench_rank_count_mismatch_is_refused():

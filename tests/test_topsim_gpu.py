@@ -242,6 +242,121 @@ def test_topsim_stretch_many_sources_per_workgroup(gw, oracle):
                 assert abs(sa - osc[r, k]) <= 1e-12 * osc[r, k]
 
 
+def _topk_match(I, S, oi, osc):
+    for r in range(len(I)):
+        m = int((oi[r] >= 0).sum())
+        got = I[r][I[r] >= 0]
+        assert len(got) == m
+        np.testing.assert_allclose(S[r, :m], osc[r, :m], rtol=1e-12)
+        omap = dict(zip(oi[r, :m].tolist(), osc[r, :m].tolist()))
+        for k, (a, b) in enumerate(zip(got.tolist(), oi[r, :m].tolist())):  # ids equal except at fp-noise ties
+            if a != b:
+                sa = omap.get(a, S[r, k])
+                assert abs(sa - osc[r, k]) <= 1e-12 * osc[r, k]
+
+
+def test_topsim_small_hash_graph_more_pair_updates_than_append_room(gw, oracle):
+    """A hash-mode graph with V just above the dense LDS row (V = 14,000: 112 KB
+    > 96 KB) at the stretch parameters SAMPLE 10000 / STEP 5: the pipelined
+    kernel runs (W/E ~ 49), touch_cap = 2^15 and the append buffer holds
+    app_cap = 16,384 updates, while a source makes ~50k-75k pair updates.
+    V <= app_cap bounds the DISTINCT keys only; the append-and-reduce choice
+    must use the uncapped pair-update bound, else the appended updates
+    overflow and the call fails with GW_ERR_CAPACITY (round-5 advisor
+    finding).  Top-100 rows, dense rows and exact counters against the oracle."""
+    import torch
+    from gwamd import _lib as Cl
+    g = gw.GWGraph.rmat_java(14_000, 350_000, 0.57, 0.19, 0.19, 42)
+    c = g.export_csr()
+    offs, nbrs = c["offsets"], c["nbrs"]
+    deg = np.diff(offs)
+    nz = np.nonzero(deg > 0)[0]
+    pick = np.concatenate([nz[np.argsort(deg[nz])[-2:]], nz[np.linspace(0, len(nz) - 1, 46).astype(np.int64)]])
+    pick = pick.astype(np.int32)
+    g.to_device(0)
+    K, sample, step = 100, 10000, 5
+    src = torch.as_tensor(pick, device="cuda")
+    ids = torch.empty((len(pick), K), dtype=torch.int32, device="cuda")
+    sc = torch.empty((len(pick), K), dtype=torch.float64, device="cuda")
+    st = torch.zeros(4, dtype=torch.int64, device="cuda")
+    Cl.check(Cl.lib().gw_topsim(g.handle, 0, sample, step, 0.6, 42, Cl.ptr(src), len(pick), K, Cl.ptr(ids),
+                                Cl.ptr(sc), Cl.ptr(st), None), g.handle)
+    assert Cl.lib().gw_topsim_kernel(g.handle) == b"k_topsim_pipe<5>"
+    oi, osc, ost = oracle.topsim_topk(offs, nbrs, 0, sample, step, K, C=0.6, seed=42, sources=pick, nthreads=8)
+    stg = st.cpu().numpy()
+    assert int(stg[0]) == ost["extensions"] and int(stg[1]) == ost["pair_updates"]
+    assert int(stg[3]) == ost["walkers"]
+    assert ost["pair_updates"] > 16384 * len(pick)  # more updates per source than the append buffer holds
+    _topk_match(ids.cpu().numpy(), sc.cpu().numpy(), oi, osc)
+    rows = torch.empty((len(pick), len(deg)), dtype=torch.float64, device="cuda")
+    st.zero_()
+    Cl.check(Cl.lib().gw_topsim_dense(g.handle, 0, sample, step, 0.6, 42, Cl.ptr(src), len(pick), Cl.ptr(rows),
+                                      Cl.ptr(st), None), g.handle)
+    ref, rst = oracle.topsim(offs, nbrs, 0, sample, step, C=0.6, seed=42, sources=pick, nthreads=8)
+    R = rows.cpu().numpy()
+    np.testing.assert_allclose(R, ref, rtol=1e-12, atol=1e-12 * sample)
+    assert np.array_equal(R > 0, ref > 0)
+    assert int(st[1]) == rst["pair_updates"]
+
+
+def test_topsim_stretch_heavy_sources_sparse_and_dense_rows(gw, oracle):
+    """Sparse rows (gw_topsim_sparse, the Java-exact writer's input) and dense
+    rows on the pipelined kernel with append-and-reduce sources: the 1M-vertex
+    Java R-MAT at SAMPLE 10000 / STEP 5, the two hubs and six strided sources
+    (each makes ~50k pair updates: over 2x the LDS load limit and within the
+    131,072-entry append buffer).  Rows against the oracle's dense rows
+    (rtol 1e-12, identical support) and exact counters; the capacity
+    protocol of the sparse rows (too small -> GW_ERR_CAPACITY, *used = room
+    needed)."""
+    import torch
+    from gwamd import _lib as Cl
+    g = gw.GWGraph.rmat_java(1_000_000, 10_000_000, 0.57, 0.19, 0.19, 42)
+    c = g.export_csr()
+    offs, nbrs = c["offsets"], c["nbrs"]
+    n = len(offs) - 1
+    deg = np.diff(offs)
+    nz = np.nonzero(deg > 0)[0]
+    pick = np.concatenate([nz[np.argsort(deg[nz])[-2:]], nz[np.linspace(0, len(nz) - 1, 6).astype(np.int64)]])
+    pick = pick.astype(np.int32)
+    g.to_device(0)
+    sample, step = 10000, 5
+    src = torch.as_tensor(pick, device="cuda")
+    ref, rst = oracle.topsim(offs, nbrs, 0, sample, step, C=0.6, seed=42, sources=pick, nthreads=8)
+
+    def sparse(capacity):
+        b = torch.empty(len(pick), dtype=torch.int64, device="cuda")
+        ln = torch.empty(len(pick), dtype=torch.int32, device="cuda")
+        ids = torch.empty(max(capacity, 1), dtype=torch.int32, device="cuda")
+        sc = torch.empty(max(capacity, 1), dtype=torch.float64, device="cuda")
+        used = torch.zeros(1, dtype=torch.int64, device="cuda")
+        st = torch.zeros(4, dtype=torch.int64, device="cuda")
+        rc = Cl.lib().gw_topsim_sparse(g.handle, 0, sample, step, 0.6, 42, Cl.ptr(src), len(pick), capacity,
+                                       Cl.ptr(b), Cl.ptr(ln), Cl.ptr(ids), Cl.ptr(sc), Cl.ptr(used), Cl.ptr(st), None)
+        return rc, b.cpu().numpy(), ln.cpu().numpy(), ids.cpu().numpy(), sc.cpu().numpy(), int(used.cpu()[0]), \
+            st.cpu().numpy()
+
+    rc, b, ln, ids, sc, used, st = sparse(20000)
+    assert rc == Cl.GW_ERR_CAPACITY and used > 20000
+    rc, b, ln, ids, sc, used2, st = sparse(used)
+    assert rc == 0 and used2 == used and int(ln.sum()) == used
+    assert Cl.lib().gw_topsim_kernel(g.handle) == b"k_topsim_pipe<5>"
+    assert int(st[0]) == rst["extensions"] and int(st[1]) == rst["pair_updates"] and int(st[3]) == rst["walkers"]
+    for r in range(len(pick)):
+        row_ids = ids[b[r]:b[r] + ln[r]]
+        assert len(np.unique(row_ids)) == ln[r]
+        nzr = np.nonzero(ref[r])[0]
+        assert np.array_equal(np.sort(row_ids), nzr)
+        np.testing.assert_allclose(sc[b[r]:b[r] + ln[r]], ref[r][row_ids], rtol=1e-12, atol=0)
+    rows = torch.empty((len(pick), n), dtype=torch.float64, device="cuda")
+    st2 = torch.zeros(4, dtype=torch.int64, device="cuda")
+    Cl.check(Cl.lib().gw_topsim_dense(g.handle, 0, sample, step, 0.6, 42, Cl.ptr(src), len(pick), Cl.ptr(rows),
+                                      Cl.ptr(st2), None), g.handle)
+    R = rows.cpu().numpy()
+    np.testing.assert_allclose(R, ref, rtol=1e-12, atol=0)
+    assert np.array_equal(R > 0, ref > 0)
+    assert int(st2[1]) == rst["pair_updates"]
+
+
 def test_mirror_compute_and_print(gw, oracle, tmp_path):
     """TopSim_singleSample mirror + printByOrder on GPU dense rows == Java
     emulation over the oracle rows."""

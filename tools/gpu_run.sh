@@ -64,6 +64,7 @@ for step in "$@"; do
         python bench.py --no-cpu-baseline $BENCH_ARGS > "$O/kt_$TAG.json" 2> "$O/kt_$TAG.err" ||
         step_fail kt $? "$O/kt_$TAG.err"
       python tools/kt_summary.py "$O/kt_$TAG/kt_kernel_trace.csv" "$O/kt_$TAG/kernel_dispatch_summary.json" > /dev/null || true
+      python tools/kt_lines.py "$O/kt_$TAG/kt_kernel_trace.csv" "$O/kt_$TAG.json" "$O/kt_$TAG/kt_lines.json" > /dev/null || true
       echo "STEP_OK kt" ;;
     pmc)
       i=0

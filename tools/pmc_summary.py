@@ -42,10 +42,21 @@ def rows(d):
     return out
 
 
-def mean_counter(rs, counter, kre, grid):
-    v = [float(r["Counter_Value"]) for r in rs
-         if r["Counter_Name"] == counter and re.match(kre, norm(r["Kernel_Name"]))
+def matching(rs, kre, grid, nth=None):
+    """Rows of the dispatches a line measured: kernel regex and grid, and with
+    `nth` only those dispatches' ordinals among the regex's matches in
+    dispatch order (bench.py ts_dispatch: lines sharing one kernel)."""
+    m = [r for r in rs if re.match(kre, norm(r["Kernel_Name"]))
          and (grid is None or int(r.get("Grid_Size", -1)) == grid)]
+    if nth is not None:
+        ids = sorted({int(r["Dispatch_Id"]) for r in m})
+        keep = {ids[k] for k in nth if k < len(ids)}
+        m = [r for r in m if int(r["Dispatch_Id"]) in keep]
+    return m
+
+
+def mean_counter(rs, counter, kre, grid, nth=None):
+    v = [float(r["Counter_Value"]) for r in matching(rs, kre, grid, nth) if r["Counter_Name"] == counter]
     return (sum(v) / len(v), len(v)) if v else (None, 0)
 
 
@@ -60,7 +71,7 @@ def lines(bench):
     yield from of(bench)
     for v in (bench.get("secondary") or {}).values():
         yield from of(v)
-        for m in (v or {}).get("more", []) or []:
+        for m in ((v or {}).get("more", []) or []) + ((v or {}).get("points", []) or []):
             yield from of(m)
 
 
@@ -78,18 +89,21 @@ def main():
         tag, m = roof.get("pmc_tag"), roof.get("pmc_match")
         if not tag or not m:
             continue
-        kre, grid = m["kernel"], m.get("grid")
-        fb, nf = mean_counter(F, "FETCH_SIZE", kre, grid)
-        wb, nw = mean_counter(W, "WRITE_SIZE", kre, grid)
-        rq, nr = mean_counter(R, "TCC_EA0_RDREQ_sum", kre, grid)
-        hit, _ = mean_counter(R, "TCC_HIT_sum", kre, grid)
-        miss, _ = mean_counter(R, "TCC_MISS_sum", kre, grid)
+        kre, grid, nth = m["kernel"], m.get("grid"), m.get("nth")
+        fb, nf = mean_counter(F, "FETCH_SIZE", kre, grid, nth)
+        wb, nw = mean_counter(W, "WRITE_SIZE", kre, grid, nth)
+        rq, nr = mean_counter(R, "TCC_EA0_RDREQ_sum", kre, grid, nth)
+        hit, _ = mean_counter(R, "TCC_HIT_sum", kre, grid, nth)
+        miss, _ = mean_counter(R, "TCC_MISS_sum", kre, grid, nth)
+        sel = matching(F, kre, grid, nth)
         if fb is None or wb is None:
             print(f"{tag}: no matching dispatches for {kre} grid {grid}", file=sys.stderr)
             continue
         units = roof.get("units_per_launch")
         e = {
-            "kernel": kre, "grid": grid, "dispatches": [nf, nw, nr], "lib_sha256": sha,
+            "kernel": kre, "grid": grid, "nth": nth, "dispatches": [nf, nw, nr], "lib_sha256": sha,
+            "scratch_bytes": max(int(r.get("Scratch_Size") or 0) for r in sel) if sel else None,
+            "vgprs": max(int(r.get("VGPR_Count") or 0) for r in sel) if sel else None,
             "units_per_launch": units,
             "fetch_bytes_per_launch": fb * 1024, "write_bytes_per_launch": wb * 1024,
             "hbm_bytes_per_launch": 2 * fb * 1024 + wb * 1024,
