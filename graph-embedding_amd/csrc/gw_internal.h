@@ -119,7 +119,9 @@ struct gw_topsim_ws {
   double* ov_list = nullptr;      // [blocks][touch_cap] compacted overflow values of a source (hash mode)
   int32_t* touched = nullptr;     // [blocks][touch_cap] claimed overflow slots
   int64_t app_cap = 0;            // pipelined hash mode: appended pair updates per source (heavy sources)
-  double* app = nullptr;          // [blocks][2][app_cap] 16 B entries {int32 key, pad, f64 value}: appended, partitioned
+  double* app = nullptr;          // [blocks][2 app_cap] 16 B entries {int32 key, pad, f64 value}: a heavy source's partitions
+  int32_t* claim = nullptr;       // [blocks][touch_cap] a heavy source's claimed overflow-hash slots
+  long long* redo = nullptr;      // [5] the caller's stats / sparse cursor before a launch that may be re-run
   int pipe = 0;                   // pipelined kernel (levels of the next source built by wave 0 during
                                   // the walkers): level / spawner scratch doubled per workgroup
   int diag_pipe = -1;             // -DGW_DIAG builds: the GW_DIAG_TS_PIPE_MAX override the workspace was made for

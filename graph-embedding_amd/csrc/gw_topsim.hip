@@ -87,9 +87,12 @@ struct TsArgs {
   int32_t* dsel_id;  // pipelined kernel, top-k rows: a source's selected entries awaiting order, [blocks][TOPK_MAX]
   double* dsel_val;
   int32_t* touched;
-  double* app;         // pipelined hash mode: [blocks][2][app_cap] 16 B entries (appended, partitioned)
+  double* app;         // pipelined hash mode: [blocks][2 app_cap] 16 B entries: a heavy source's key-hash partitions
   int64_t app_cap;     // 0: no append-and-reduce path
   int64_t heavy_min;   // a source appends past the LDS table when its pair-update bound exceeds this
+  int32_t* claim;      // [blocks][touch_cap] a heavy source's claimed overflow-hash slots
+  int part_entries;    // a heavy source gets the power of two of partitions that keeps its bound <= this each
+  int pcap_shrink;     // -DGW_DIAG only (GW_DIAG_TS_PCAP_SHRINK): partitions 2^-k of their room, to force flag 8
   unsigned int* src_counter;
   int* error_flag;
   unsigned long long* phase;  // diagnostics (GW_DIAG_TS_PHASES): cycles per phase, thread 0 of each block
@@ -270,6 +273,7 @@ struct TsPipeMeta {
   int nspawn, nwalk, ncontrib;
   uint32_t ovmask;  // slots - 1 of the source's overflow hash (hash mode)
   int heavy;        // append-and-reduce past the LDS table (hash mode)
+  int plg;          // log2 of its key-hash partitions
   int valid;
 };
 
@@ -504,6 +508,9 @@ __device__ __forceinline__ TsLevelStats ts_wave_levels(const TsArgs& A, int b, i
       while (t < ub + ub / 8 + 1 && t < A.touch_cap) t <<= 1;
       s_pm[b].ovmask = (uint32_t)(t - 1);
       s_pm[b].heavy = A.app_cap > 0 && pairs > A.heavy_min && pairs <= A.app_cap && !(kGwDiag && (A.diag & (32768 | 8192)));
+      int lg = 0;
+      while (((int64_t)A.part_entries << lg) < pairs && lg < 6) ++lg;
+      s_pm[b].plg = lg;
       s_pm[b].valid = 1;
     }
   }
@@ -540,8 +547,10 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   __shared__ int s_src, s_nspawn, s_nwalk, s_ntouch, s_cnt, s_need, s_abort, s_hcount, s_bin, s_cum, s_exact, s_total,
       s_ncomp, s_all, s_novc;
   __shared__ uint32_t s_ovmask;  // the slots (minus 1) of this source's overflow hash
-  __shared__ int s_heavy, s_napp;  // append-and-reduce source; pair updates appended
-  __shared__ int s_pbase[65], s_pcur[64];  // its partitions' offsets / fill cursors
+  __shared__ int s_heavy, s_plg;  // append-and-reduce source; log2 of its key-hash partitions
+  __shared__ int s_pinfo;          // s_plg | log2(entries per partition) << 8
+  __shared__ int s_hdone;          // LDS-table reservations whose CAS has completed (the key set is final at HASH_LIMIT)
+  __shared__ int s_pcur[64];       // its partitions' fill counts
   __shared__ unsigned long long s_prefix, s_mask, s_spbase;
   // the output phase's selection arrays share LDS with the levels' child
   // offsets / the walkers' spawner offsets (binary-searched per child / walker)
@@ -600,10 +609,19 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   // (register allocation), and a STEP-3 source over the LDS table keeps the
   // HBM hash (profiles/r05/tsab_r05s*, tsab_r05t*).
   constexpr bool APPEND = PIPE && STEP >= 4;
-  auto app_base = [&](int buf) -> double* {
-    int64_t o = (4 * blk + 2 * buf) * A.app_cap;
+  auto app_base = [&]() -> double* {  // [2 app_cap] 16 B entries: partition p at entries [p cap_p, (p+1) cap_p)
+    int64_t o = 4 * blk * A.app_cap;
     asm volatile("" : "+s"(o));
     return A.app + o;
+  };
+  auto claim_base = [&]() -> int32_t* {
+    int64_t o = blk * A.touch_cap;
+    asm volatile("" : "+s"(o));
+    return A.claim + o;
+  };
+  // key-hash partition of a heavy source's key (lg = log2 of its partitions)
+  auto part_of = [](int32_t key, int lg) -> int {
+    return lg ? (int)(((uint32_t)key * 0x85EBCA77u) >> (32 - lg)) : 0;
   };
   // the slots a source's overflow hash uses: all touch_cap of them, or (PIPE)
   // the power of two above the source's own bound on distinct overflow keys,
@@ -636,8 +654,11 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     s_hcount = 0;
     s_ovmask = (uint32_t)(A.touch_cap - 1);
     s_heavy = 0;
-    s_napp = 0;
+    s_plg = 0;
+    s_pinfo = 0;
+    s_hdone = 0;
   }
+  if (tid < 64) s_pcur[tid] = 0;
   __syncthreads();
 
   // overflow insert into the workgroup's HBM hash (slots claimed by CAS; the
@@ -652,7 +673,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         if (old == -1) {
           const int k = atomicAdd(&s_ntouch, 1);
           if ((int64_t)k >= A.touch_cap * 3 / 4) atomicOr(A.error_flag, 2);
-          else if (!(APPEND && s_heavy)) touched[k] = (int32_t)h;  // (heavy: compacted by the slot scan)
+          else if (APPEND && s_heavy) claim_base()[k] = (int32_t)h;  // (heavy: merged and compacted from the claims)
+          else touched[k] = (int32_t)h;
         }
         atomicAdd(&ov_val[2 * h + 1], val);
         return;
@@ -725,24 +747,54 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         // one LDS address)
         if ((APPEND && s_hcount >= HASH_LIMIT) || atomicAdd(&s_hcount, 1) >= HASH_LIMIT) break;
         const int32_t old = atomicCAS(&s_hkey[h], -1, target);
-        if (old == -1 || old == target) {
+        const bool mine = old == -1 || old == target;
+        if (APPEND) atomicAdd(&s_hdone, 1);  // (after the CAS has returned)
+        if (mine) {
           atomicAdd(&s_hval[h], val);
           return;
         }
       }
       h = H::next(h);
     }
-    if (APPEND && s_heavy) {  // append-and-reduce source: appended, reduced in the output phase
-      const int k = atomicAdd(&s_napp, 1);
-      if ((int64_t)k < A.app_cap) {
-        double* ab = app_base(0);
-        reinterpret_cast<int32_t*>(ab)[4 * k] = target;
-        ab[2 * k + 1] = val;
+    if (APPEND && s_heavy && s_hdone >= HASH_LIMIT) {
+      // append-and-reduce source whose LDS table is final (every reserved
+      // insert has landed).  Slots never empty and keys never change, so the
+      // key, if an insert racing this probe placed it, sits at or after the
+      // empty slot the probe stopped at (an insert takes its chain's first
+      // empty slot): finish the check there — one LDS read unless that slot
+      // filled meanwhile.
+      for (int probe = 0; probe < HASH_SLOTS; ++probe) {
+        const int32_t k = s_hkey[h];
+        if (k == target) {
+          atomicAdd(&s_hval[h], val);
+          return;
+        }
+        if (k == -1) break;
+        h = H::next(h);
+      }
+      // not in the table: appended to its key-hash partition, reduced per
+      // partition in the output phase
+      // (32-bit: 2 app_cap = touch_cap entries, a power of two; partition p
+      // holds 2^cs of them from entry p 2^cs)
+      const int pi = s_pinfo;
+      const int lg = pi & 255, cs = pi >> 8;
+      const uint32_t p = lg ? ((uint32_t)target * 0x85EBCA77u) >> (32 - lg) : 0u;
+      const int k = atomicAdd(&s_pcur[p], 1);
+      if (k < (1 << cs)) {
+        double* ab = app_base();
+        const uint32_t e = (p << cs) + (uint32_t)k;
+        reinterpret_cast<int32_t*>(ab)[4 * e] = target;
+        ab[2 * e + 1] = val;
       } else {
-        atomicOr(A.error_flag, 2);
+        // a partition past 2x its share (one key with thousands of updates
+        // that missed the table): the host re-runs the launch without the
+        // append path (flag 8)
+        atomicOr(A.error_flag, 8);
       }
       return;
     }
+    // (heavy: an update made before the table's last inserts landed goes to
+    // the HBM hash; the output phase merges its keys with the tables)
     ov_add(target, val);
   };
 
@@ -787,14 +839,14 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     }
   };
 
-  __shared__ unsigned long long s_ph[11];  // diagnostics only: [10] = last timestamp
+  __shared__ unsigned long long s_ph[16];  // diagnostics only: [15] = last timestamp
   if (tid == 0)
-    for (int k = 0; k < 11; ++k) s_ph[k] = 0;
+    for (int k = 0; k < 16; ++k) s_ph[k] = 0;
   auto mark = [&](int k) {
     if (kGwDiag && A.phase && tid == 0) {
       const unsigned long long now = __builtin_readcyclecounter();
-      if (k >= 0) s_ph[k] += now - s_ph[10];
-      s_ph[10] = now;
+      if (k >= 0) s_ph[k] += now - s_ph[15];
+      s_ph[15] = now;
     }
   };
   // one walker (index g in the reference's BFS queue order) of source s from
@@ -921,7 +973,8 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         s_novc = 0;
         if (!LDS_ROW) s_ovmask = s_pm[cur].ovmask;
         s_heavy = (APPEND && !LDS_ROW) ? s_pm[cur].heavy : 0;
-        s_napp = 0;
+        s_plg = s_pm[cur].plg;
+        s_pinfo = s_plg | ((31 - __builtin_clz((uint32_t)A.touch_cap) - s_plg - (kGwDiag ? A.pcap_shrink : 0)) << 8);
       }
       __syncthreads();
     } else {
@@ -1137,16 +1190,16 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     // (counter-limited table: the chain ends at an empty slot; diag 8192: within kTsProbeCap slots)
     const int fold_cap = (kGwDiag && (A.diag & 8192)) ? kTsProbeCap : HASH_SLOTS;
     // the key's LDS chain, four keys per ds_read_b128, up to its first empty slot
-    auto fold_lds = [&](int32_t key, double& v) {
+    auto fold_lds = [&](int32_t key, double& v, int cap) {
       uint32_t h = H::slot(key);
       bool done = false;
-      for (int probed = 0; probed < fold_cap && !done;) {
+      for (int probed = 0; probed < cap && !done;) {
         const uint32_t g0 = h & ~3u;
         const int4 kv = *reinterpret_cast<const int4*>(&s_hkey[g0]);
         const int32_t ks[4] = {kv.x, kv.y, kv.z, kv.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if (done || (uint32_t)j < (h & 3u) || probed >= fold_cap) continue;
+          if (done || (uint32_t)j < (h & 3u) || probed >= cap) continue;
           ++probed;
           if (ks[j] == -1) {
             done = true;
@@ -1200,86 +1253,120 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         }
     };
     // append-and-reduce source (PIPE, hash mode; wave 0's level build bounds its
-    // pair updates above heavy_min): the updates that found no room in the LDS
-    // table were appended (16 B each, streamed) instead of going one random
-    // CAS line each to the HBM hash.  Here: (1) appended keys that reached the
-    // LDS table anyway (the load-limit race) are folded into it, the rest
-    // counted per key-hash partition (<= 3584 entries each); (2) they are
-    // scattered into their partitions while the LDS table moves to the
-    // candidate list; (3) each partition is reduced in the emptied LDS table
-    // (counter-free insert; a key with no room within kTsProbeCap slots goes
-    // to the HBM hash, which the slot scan below compacts) and moved to the
-    // candidate list.  The selection then reads the list only.
+    // pair updates above heavy_min): an update whose key is not in the full
+    // LDS table was appended, during the walk, to its key-hash partition
+    // (16 B, no random CAS line in the HBM hash).  Updates that raced the
+    // table's last inserts (the key may have landed in it) and those of a
+    // full partition went to the HBM hash, whose claimed slots are listed.
+    // Here: (0) those HBM keys the LDS table holds are folded into it; the
+    // table moves to the candidate list; (1) each partition is reduced in the
+    // emptied LDS table (counter-free insert: a key without room within
+    // kTsProbeCap slots goes to the HBM hash), the HBM keys of that partition
+    // are folded into it, and it moves to the candidate list; (2) the HBM
+    // keys left are compacted into the list.  A key thus ends in exactly one
+    // candidate entry; the selection reads the list only.
     const bool heavy = APPEND && !LDS_ROW && s_heavy;
     if (heavy) {
-      int32_t* app_key = reinterpret_cast<int32_t*>(app_base(0));
-      double* app_val = app_base(0);
-      int32_t* par_key = reinterpret_cast<int32_t*>(app_base(1));
-      double* par_val = app_base(1);
-      const int napp = (int)min((int64_t)s_napp, A.app_cap);
-      int lg = 0;
-      while ((3584 << lg) < napp && lg < 6) ++lg;
+      const int lg = s_plg;
       const int NP = 1 << lg;
-      auto part = [&](int32_t key) -> int {
-        return lg ? (int)(((uint32_t)key * 0x85EBCA77u) >> (32 - lg)) : 0;
-      };
-      if (tid < 64) s_pcur[tid] = 0;
-      __syncthreads();
-      for (int k = tid; k < napp; k += BLOCK) {  // (1)
-        const int32_t key = app_key[4 * k];
-        double v = app_val[2 * k + 1];
-        fold_lds(key, v);
-        if (v == 0.0)  // folded (pair updates are > 0)
-          app_key[4 * k] = -1;
-        else
-          atomicAdd(&s_pcur[part(key)], 1);
+      const int64_t cap_p = (int64_t)1 << (s_pinfo >> 8);  // == 2 app_cap >> lg
+      const int32_t* bkey = reinterpret_cast<const int32_t*>(app_base());
+      const double* bval = app_base();
+      int32_t* cl = claim_base();
+      const int cap34 = (int)(A.touch_cap * 3 / 4);
+      mark(13);
+      // (0) claimed HBM keys held by the LDS table (a folded entry keeps its key
+      // for the probe chains; value 0 marks it: pair updates are > 0)
+      int nt = min(s_ntouch, cap34);
+      for (int k = tid; k < nt; k += BLOCK) {
+        const int32_t slot = cl[k];
+        const int32_t key = __hip_atomic_load(&ov_key[4 * slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        double v = __hip_atomic_load(&ov_val[2 * slot + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fold_lds(key, v, fold_cap);
+        if (v == 0.0) __hip_atomic_store(&ov_val[2 * slot + 1], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
-      if (tid < 64) {  // exclusive scan of the NP <= 64 partition sizes
-        int lane = tid;
-        asm volatile("" : "+v"(lane));
-        const int c = s_pcur[lane];
-        int incl = c;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const int y = __shfl_up(incl, d, 64);
-          if (lane >= d) incl += y;
-        }
-        s_pbase[lane] = incl - c;
-        s_pcur[lane] = incl - c;
-        if (lane == 63) s_pbase[64] = incl;
-      }
-      __syncthreads();
-      for (int k = tid; k < napp; k += BLOCK) {  // (2)
-        const int32_t key = app_key[4 * k];
-        if (key == -1) continue;
-        const int pos = atomicAdd(&s_pcur[part(key)], 1);
-        par_key[4 * pos] = key;
-        par_val[2 * pos + 1] = app_val[2 * k + 1];
-      }
       dump_lds();
       __syncthreads();
-      for (int p = 0; p < NP; ++p) {  // (3)
-        const int b1 = s_pbase[p + 1];
-        for (int k = s_pbase[p] + tid; k < b1; k += BLOCK) {
-          const int32_t key = par_key[4 * k];
-          const double v = par_val[2 * k + 1];
-          if (!cf_insert(key, v)) ov_add(key, v);
+      mark(10);  // diagnostics: claims folded into the table + table dump
+      for (int p = 0; p < NP; ++p) {  // (1)
+        const int np = (int)min((int64_t)s_pcur[p], cap_p);
+        const int64_t e0 = (int64_t)p * cap_p;
+        constexpr int U = 8;  // eight entries per thread and round: their reads issued together
+        for (int k0 = tid; k0 < np; k0 += U * BLOCK) {
+          int32_t key[U];
+          double v[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int k = k0 + u * BLOCK;
+            key[u] = k < np ? bkey[4 * (e0 + k)] : -1;
+            v[u] = k < np ? bval[2 * (e0 + k) + 1] : 0.0;
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (key[u] != -1 && !cf_insert(key[u], v[u])) ov_add(key[u], v[u]);
         }
         __syncthreads();
+        nt = min(s_ntouch, cap34);
+        if (nt > 0) {  // this partition's claimed HBM keys held by its table
+          for (int k = tid; k < nt; k += BLOCK) {
+            const int32_t slot = cl[k];
+            const int32_t key = __hip_atomic_load(&ov_key[4 * slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (part_of(key, lg) != p) continue;
+            double v = __hip_atomic_load(&ov_val[2 * slot + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (v == 0.0) continue;
+            fold_lds(key, v, kTsProbeCap);  // (counter-free table: a key sits within its first kTsProbeCap slots)
+            if (v == 0.0) __hip_atomic_store(&ov_val[2 * slot + 1], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          __syncthreads();
+        }
         dump_lds();
         __syncthreads();
       }
+      mark(11);  // diagnostics: partition reduces
+      // (2) the claimed HBM keys no table held -> the candidate list; every claimed slot cleared
+      nt = min(s_ntouch, cap34);
+      const int lane = tid & 63;
+      const unsigned long long below = (1ull << lane) - 1ull;
+      for (int k0 = 0; k0 < nt; k0 += BLOCK) {
+        const int k = k0 + tid;
+        int32_t key = -1;
+        double v = 0.0;
+        if (k < nt) {
+          const int32_t slot = cl[k];
+          key = __hip_atomic_load(&ov_key[4 * slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v = __hip_atomic_load(&ov_val[2 * slot + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&ov_key[4 * slot], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&ov_val[2 * slot + 1], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const bool keep = v != 0.0;
+        const unsigned long long m = __ballot(keep);
+        int wbase = 0;
+        if (lane == 0 && m) wbase = atomicAdd(&s_novc, __popcll(m));
+        wbase = __shfl(wbase, 0, 64);
+        if (keep) {
+          const int o = wbase + __popcll(m & below);
+          if (o < cap34) {
+            __hip_atomic_store(&touched[o], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ov_list[o], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            atomicOr(A.error_flag, 2);
+          }
+        }
+      }
+      __syncthreads();
+      nov = min(s_novc, cap34);
       if (tid == 0) s_hcount = 0;
+      mark(12);  // diagnostics: claims compaction
     }
     // a source with many overflow keys for its table (>= 1/8 of the slots)
     // compacts by scanning the slots in order: coalesced reads and clears
     // instead of two random line accesses per key through `touched` (an
     // append-and-reduce source always: its list is the candidate list)
     const uint32_t ov_mask = s_ovmask;
-    const bool ov_scan = !LDS_ROW && s_ntouch > 0 &&
-                         (heavy || ((int64_t)s_ntouch * 8 >= (int64_t)ov_mask + 1 &&
-                                    !(kGwDiag && (A.diag & 16384))));  // diag bit 16384: always through `touched` (A/B)
+    const bool ov_scan = !LDS_ROW && !heavy && s_ntouch > 0 &&
+                         (int64_t)s_ntouch * 8 >= (int64_t)ov_mask + 1 &&
+                         !(kGwDiag && (A.diag & 16384));  // diag bit 16384: always through `touched` (A/B)
     if (ov_scan) {
       const int T = (int)ov_mask + 1;
       const int cap34 = (int)(A.touch_cap * 3 / 4);
@@ -1318,7 +1405,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           const int i = b0 + u * BLOCK + ti;
           __hip_atomic_store(&ov_key[4 * i], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&ov_val[2 * i + 1], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          fold_lds(key[u], v[u]);
+          fold_lds(key[u], v[u], fold_cap);
           const int k = wbase + pre[u];
           if (k < cap34) {
             __hip_atomic_store(&touched[k], key[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1330,9 +1417,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       }
       __syncthreads();
       nov = min(s_novc, cap34);
-    } else if (heavy) {
-      nov = min(s_novc, (int)(A.touch_cap * 3 / 4));
-    } else if (!LDS_ROW && nov > 0) {
+    } else if (!LDS_ROW && !heavy && nov > 0) {
       // four entries per thread and round, their slot reads issued together
       // (the stretch compacts ~31k entries per source: the loop was a chain of
       // dependent random reads per entry)
@@ -1359,7 +1444,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           if (slot[u] < 0) continue;
           __hip_atomic_store(&ov_key[4 * slot[u]], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&ov_val[2 * slot[u] + 1], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          fold_lds(key[u], v[u]);
+          fold_lds(key[u], v[u], fold_cap);
           const int k = k0 + u * BLOCK;
           __hip_atomic_store(&touched[k], key[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&ov_list[k], v[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1443,6 +1528,29 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       }
       return *val > 0.0;
     };
+    // f(id, value) for this thread's candidates idx = tid, tid + BLOCK, ... < NC
+    // with a value > 0; the loads of kCandBatch of them are issued together
+    // (the overflow list sits in L2 / HBM: a pass over ~36k stretch candidates
+    // was ~70 dependent round trips per thread, one per entry)
+    // (the append-and-reduce kernels only, whose heavy sources keep ~36k
+    // candidates in the list: the unpipelined arxiv kernel measured +2.7% with
+    // the batch, the others +-0; profiles/r06/tsab_r06e.jsonl)
+    constexpr int kCandBatch = APPEND ? 8 : 1;
+    auto for_cands = [&](auto&& f) {
+      for (int b0 = tid; b0 < NC; b0 += kCandBatch * BLOCK) {
+        int32_t id[kCandBatch];
+        double v[kCandBatch];
+#pragma unroll
+        for (int u = 0; u < kCandBatch; ++u) {
+          id[u] = 0;
+          v[u] = 0.0;
+          if (b0 + u * BLOCK < NC) cand(b0 + u * BLOCK, &id[u], &v[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kCandBatch; ++u)
+          if (v[u] > 0.0) f(id[u], v[u]);
+      }
+    };
     if (A.out_rows) {
       double* orow = A.out_rows + r * (int64_t)n;
       // (an opaque copy of tid: its row addresses are not hoisted out of the
@@ -1454,11 +1562,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       } else {
         for (int t = t0; t < n; t += BLOCK) orow[t] = 0.0;
         __syncthreads();
-        for (int idx = tid; idx < NC; idx += BLOCK) {
-          int32_t id;
-          double v;
-          if (cand(idx, &id, &v)) orow[id] = v;
-        }
+        for_cands([&](int32_t id, double v) { orow[id] = v; });
       }
     }
     if (A.sp.cursor) {
@@ -1466,11 +1570,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       // claimed offset; a row that does not fit is skipped (len -1) but still
       // counted, so the cursor ends at the room all rows need
       int mine = 0;
-      for (int idx = tid; idx < NC; idx += BLOCK) {
-        int32_t id;
-        double v;
-        mine += cand(idx, &id, &v) ? 1 : 0;
-      }
+      for_cands([&](int32_t, double) { ++mine; });
       int tot;
       const int ex = block_excl_scan<NW>(mine, s_wave, &tot);
       if (tid == 0) s_spbase = atomicAdd(A.sp.cursor, (unsigned long long)tot);
@@ -1479,15 +1579,11 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       const bool fits = base + tot <= A.sp.cap;
       if (fits) {
         int64_t o = base + ex;
-        for (int idx = tid; idx < NC; idx += BLOCK) {
-          int32_t id;
-          double v;
-          if (cand(idx, &id, &v)) {
-            A.sp.ids[o] = id;
-            A.sp.scores[o] = v;
-            ++o;
-          }
-        }
+        for_cands([&](int32_t id, double v) {
+          A.sp.ids[o] = id;
+          A.sp.scores[o] = v;
+          ++o;
+        });
       }
       if (tid == 0) {
         A.sp.begin[r] = fits ? base : -1;
@@ -1530,13 +1626,10 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
             const unsigned long long k = dkey(v);
             if ((k & msk) == pre) atomicAdd(&H[(k >> shift) & 255], 1u);
           });
-          for (int idx = tid; idx < NC; idx += BLOCK) {
-            int32_t id;
-            double v;
-            if (!cand(idx, &id, &v)) continue;
+          for_cands([&](int32_t, double v) {
             const unsigned long long k = dkey(v);
             if ((k & msk) == pre) atomicAdd(&H[(k >> shift) & 255], 1u);
-          }
+          });
           __syncthreads();
           if (tid < 64) {
             select_bin(H, s_need, true, &s_bin, &s_cum, shift == 56 ? &s_total : nullptr);
@@ -1569,11 +1662,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         // ties at the threshold: smallest ids first
         long long eq_local = 0;
         each_reg([&](int, double v) { eq_local += dkey(v) == T; });
-        for (int idx = tid; idx < NC; idx += BLOCK) {
-          int32_t id;
-          double v;
-          if (cand(idx, &id, &v) && dkey(v) == T) ++eq_local;
-        }
+        for_cands([&](int32_t, double v) { eq_local += dkey(v) == T; });
         const int EQ = (int)block_sum<long long, NW>(eq_local, s_red);
         if (EQ > s_need) {
           if (tid == 0) {
@@ -1590,13 +1679,11 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
               const unsigned long long k = (unsigned)s_hkey[tid + i * BLOCK];
               if ((k & msk) == pre) atomicAdd(&s_hist[(k >> shift) & 255], 1u);
             });
-            for (int idx = tid; idx < NC; idx += BLOCK) {
-              int32_t id;
-              double v;
-              if (!cand(idx, &id, &v) || dkey(v) != T) continue;
+            for_cands([&](int32_t id, double v) {
+              if (dkey(v) != T) return;
               const unsigned long long k = (unsigned)id;
               if ((k & msk) == pre) atomicAdd(&s_hist[(k >> shift) & 255], 1u);
-            }
+            });
             __syncthreads();
             if (tid < 64) select_bin(s_hist, s_need, false, &s_bin, &s_cum);
             __syncthreads();
@@ -1640,24 +1727,18 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           append(vv[i] > 0.0 && selected(id, vv[i]), id, vv[i]);
         }
       }
-      for (int base = 0; base < NC; base += BLOCK) {
-        const int idx = base + tid;
-        int32_t id = 0;
-        double v = 0.0;
-        bool sel = false;
-        if (idx < NC && cand(idx, &id, &v)) sel = selected(id, v);
-        const unsigned long long sm = __ballot(sel);
-        if (sm) {
-          int wb = 0;
-          if ((tid & 63) == __ffsll(sm) - 1) wb = atomicAdd(&s_cnt, __popcll(sm));
-          wb = __shfl(wb, __ffsll(sm) - 1, 64);
-          const int slot = wb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-          if (sel && slot < TOPK_MAX) {
-            s_sel_id[slot] = id;
-            s_sel_val[slot] = v;
-          }
+      for (int base = 0; base < NC; base += kCandBatch * BLOCK) {  // (wave-uniform: append's ballots)
+        int32_t id[kCandBatch];
+        double v[kCandBatch];
+#pragma unroll
+        for (int u = 0; u < kCandBatch; ++u) {
+          id[u] = 0;
+          v[u] = 0.0;
+          const int idx = base + u * BLOCK + tid;
+          if (idx < NC) cand(idx, &id[u], &v[u]);
         }
+#pragma unroll
+        for (int u = 0; u < kCandBatch; ++u) append(v[u] > 0.0 && selected(id[u], v[u]), id[u], v[u]);
       }
       __syncthreads();
       const int cnt = min(s_cnt, TOPK_MAX);
@@ -1733,7 +1814,9 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     if (tid == 0) {
       s_ntouch = 0;
       s_hcount = 0;
+      s_hdone = 0;
     }
+    if (APPEND && tid < 64) s_pcur[tid] = 0;
     __syncthreads();
     mark(4);
     if (PIPE) cur ^= 1;
@@ -1741,7 +1824,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   if (defer && pend_r >= 0 && tid >= BLOCK - 64) deferred_topk();  // the workgroup's last source
 
   if (kGwDiag && A.phase && tid == 0)
-    for (int k = 0; k < 10; ++k) atomicAdd(&A.phase[k], s_ph[k]);
+    for (int k = 0; k < 15; ++k) atomicAdd(&A.phase[k], s_ph[k]);
   // statistics
   long long e = block_sum<long long, NW>(my_ext, s_red);
   long long u = block_sum<long long, NW>(my_upd, s_red);
@@ -1965,6 +2048,8 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   ws_free(t.ov_list);
   ws_free(t.touched);
   ws_free(t.app);
+  ws_free(t.claim);
+  ws_free(t.redo);
   ws_free(t.enum_tgt);
   ws_free(t.enum_val);
   ws_free(t.dsel_id);
@@ -2031,7 +2116,8 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
   const int64_t app_cap = (pipe && !lds_row) ? touch_cap / 2 : 0;
   const int64_t per_block = nb * ((int64_t)(L + 1) * level_cap * 20 + spawn_cap * 20 + 4) + 2 * level_cap * 8 +
                             (level_cap + 1) * 4 + (pipe ? 2 * enum_cap * 12 : 0) +
-                            (lds_row ? 0 : touch_cap * 28) + (pipe ? TOPK_MAX * 12 : 0) + app_cap * 32;
+                            (lds_row ? 0 : touch_cap * 28) + (pipe ? TOPK_MAX * 12 : 0) + app_cap * 32 +
+                            (app_cap > 0 ? touch_cap * 4 : 0);
   int dev_cus = 256;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, g->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
@@ -2072,7 +2158,9 @@ int gw_dev_topsim_prepare(gw_graph* g, int variant, int sample, int step, int to
     GW_HIP_TRY(hipMemset(t.acc_row, 0, sizeof(double) * 2 * blocks * touch_cap));
     GW_HIP_TRY(hipMemset2D(t.acc_row, 16, 0xFF, 4, (size_t)(blocks * touch_cap)));
   }
-  if (app_cap > 0 && (rc = ws_alloc(g, &t.app, 4 * blocks * app_cap))) return rc;
+  if (app_cap > 0 && ((rc = ws_alloc(g, &t.app, 4 * blocks * app_cap)) || (rc = ws_alloc(g, &t.claim, blocks * touch_cap)) ||
+                      (rc = ws_alloc(g, &t.redo, 5))))
+    return rc;
   t.variant = variant;
   t.sample = sample;
   t.step = step;
@@ -2157,6 +2245,13 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   A.touched = t.touched;
   A.app = t.app;
   A.app_cap = t.app ? t.app_cap : 0;
+  A.claim = t.claim;
+  A.part_entries = 3584;  // ~ the distinct keys one 6144-slot LDS fill takes comfortably
+  if (const char* pe = GW_DIAG_ENV("GW_DIAG_TS_PART"))  // A/B knob: partition size bound
+    A.part_entries = std::max(256, std::atoi(pe));
+  A.pcap_shrink = 0;
+  if (const char* pc = GW_DIAG_ENV("GW_DIAG_TS_PCAP_SHRINK"))  // test knob: partitions overflow -> re-run (flag 8)
+    A.pcap_shrink = std::min(8, std::max(0, std::atoi(pc)));
   A.heavy_min = 2 * (int64_t)(t.lds_row == 1 ? TsHash<1>::LIMIT : TsHash<2>::LIMIT);
   A.src_counter = t.src_counter;
   A.error_flag = t.error_flag;
@@ -2167,25 +2262,44 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   const char* dph = GW_DIAG_ENV("GW_DIAG_TS_PHASES");
   A.phase = nullptr;
   if (dph && dph[0] == '1') {
-    GW_HIP_TRY(hipMalloc((void**)&A.phase, 10 * sizeof(unsigned long long)));
-    GW_HIP_TRY(hipMemsetAsync(A.phase, 0, 10 * sizeof(unsigned long long), s));
+    GW_HIP_TRY(hipMalloc((void**)&A.phase, 15 * sizeof(unsigned long long)));
+    GW_HIP_TRY(hipMemsetAsync(A.phase, 0, 15 * sizeof(unsigned long long), s));
   }
-  hipError_t e = launch(step, t.lds_row, t.pipe != 0, A, blocks, t.lds_bytes, s);
-  if (e != hipSuccess) {
-    g->err = std::string("k_topsim launch: ") + hipGetErrorString(e);
-    return GW_ERR_DEVICE;
+  // a heavy source's key-hash partition can overflow only when one key that
+  // missed the LDS table takes thousands of its pair updates (flag 8): the
+  // launch is then re-run without the append path, from the caller's
+  // counters as they were (stats, sparse-row cursor: saved here)
+  const bool may_redo = A.app_cap > 0 && (A.stats || A.sp.cursor);
+  if (may_redo) {
+    if (A.stats) GW_HIP_TRY(hipMemcpyAsync(t.redo, A.stats, 4 * sizeof(long long), hipMemcpyDeviceToDevice, s));
+    if (A.sp.cursor) GW_HIP_TRY(hipMemcpyAsync(t.redo + 4, A.sp.cursor, sizeof(long long), hipMemcpyDeviceToDevice, s));
   }
   int flag = 0;
-  GW_HIP_TRY(hipMemcpyAsync(&flag, t.error_flag, sizeof(int), hipMemcpyDeviceToHost, s));
-  GW_HIP_TRY(hipStreamSynchronize(s));
+  for (int pass = 0; pass < 2; ++pass) {
+    hipError_t e = launch(step, t.lds_row, t.pipe != 0, A, blocks, t.lds_bytes, s);
+    if (e != hipSuccess) {
+      g->err = std::string("k_topsim launch: ") + hipGetErrorString(e);
+      return GW_ERR_DEVICE;
+    }
+    GW_HIP_TRY(hipMemcpyAsync(&flag, t.error_flag, sizeof(int), hipMemcpyDeviceToHost, s));
+    GW_HIP_TRY(hipStreamSynchronize(s));
+    if (!(flag & 8) || A.app_cap == 0) break;
+    A.app_cap = 0;  // no heavy sources: every overflow key through the HBM hash
+    if (A.stats) GW_HIP_TRY(hipMemcpyAsync(A.stats, t.redo, 4 * sizeof(long long), hipMemcpyDeviceToDevice, s));
+    if (A.sp.cursor) GW_HIP_TRY(hipMemcpyAsync(A.sp.cursor, t.redo + 4, sizeof(long long), hipMemcpyDeviceToDevice, s));
+    GW_HIP_TRY(hipMemsetAsync(t.src_counter, 0, sizeof(unsigned), s));
+    GW_HIP_TRY(hipMemsetAsync(t.error_flag, 0, sizeof(int), s));
+  }
   if (A.phase) {
-    unsigned long long ph[10];
+    unsigned long long ph[15];
     GW_HIP_TRY(hipMemcpy(ph, A.phase, sizeof ph, hipMemcpyDeviceToHost));
     (void)hipFree(A.phase);
+    const unsigned long long app = ph[10] + ph[11] + ph[12] + ph[13];
     std::fprintf(stderr, "[k_topsim phases, cycles summed over %d blocks] levels %llu walkers %llu output %llu "
-                 "(count %llu radix %llu ties %llu collect %llu order %llu) clear %llu (spawn-prefix %llu)\n",
-                 blocks, ph[0] + 0ull, ph[2], ph[3] + ph[5] + ph[6] + ph[7] + ph[8] + ph[9], ph[5], ph[6], ph[7],
-                 ph[8], ph[9], ph[4], ph[1]);
+                 "(count %llu radix %llu ties %llu collect %llu order %llu) clear %llu (spawn-prefix %llu) "
+                 "[count: append-reduce %llu = fold %llu scatter+dump %llu partitions %llu pre %llu]\n",
+                 blocks, ph[0] + 0ull, ph[2], ph[3] + ph[5] + ph[6] + ph[7] + ph[8] + ph[9] + app, ph[5] + app, ph[6],
+                 ph[7], ph[8], ph[9], ph[4], ph[1], app, ph[10], ph[11], ph[12], ph[13]);
   }
   if (flag & 3) {
     g->err = "TopSim frontier exceeded the workspace (level/spawn/touch capacity)";

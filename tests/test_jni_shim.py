@@ -16,8 +16,11 @@ called through ctypes:
   null / short arrays, a pin failure at every pin of every entry point (the
   shim releases what it pinned and returns with the OutOfMemoryError
   pending), and no input array written back;
-* GPU: load -> topsimWriteText byte-equal to gw_topsim_write_text, and
-  topsimTopK / topsimDense / simrankNaive equal to the C ABI's host calls
+* GPU: load -> topsimWriteText equal to gw_topsim_write_text on the same
+  graph (two device runs differ only by fp64-atomic summation order: ids
+  swap only at ties, %.6f strings only at an ulp-decided HALF_UP boundary),
+  topsimTopK / topsimDense equal to gw_topsim_host (rtol 1e-12) and
+  simrankNaive bitwise equal to gw_simrank_naive_host (deterministic)
   (Test_u_u_TopSim_singleSample.java:46-64's sequence).
 
 The JVM itself stays unverified (N1 "partial"): the stand-in's function-table
@@ -217,10 +220,10 @@ def test_argument_checks_and_pin_failures(jni):
 @pytest.mark.gpu
 def test_jni_gpu_driver_sequence_equals_c_abi(jni, gw, tmp_path):
     """Test_u_u_TopSim_singleSample.java:46-64 through the shim on moreno
-    (tab, V = 1380): loadGraph -> topsimWriteText byte-equal to
-    gw_topsim_write_text on the same graph; topsimTopK, topsimDense and
-    simrankNaive equal to gw_topsim_host / gw_simrank_naive_host; inputs
-    never written back; every pin released."""
+    (tab, V = 1380): loadGraph -> topsimWriteText equal to
+    gw_topsim_write_text on the same graph (up to fp64-atomic order noise);
+    topsimTopK, topsimDense and simrankNaive equal to gw_topsim_host /
+    gw_simrank_naive_host; inputs never written back; every pin released."""
     from gwamd import _lib as C
     L, O = jni, _Objs(jni)
     path = os.path.join(DATA, "moreno_crime_crime.txt")
@@ -243,8 +246,26 @@ def test_jni_gpu_driver_sequence_equals_c_abi(jni, gw, tmp_path):
         cst = np.zeros(4, np.int64)
         C.check(C.lib().gw_topsim_write_text(G.handle, 0, sample, step, 0.6, seed, C.ptr(src), ns, topk, cp.encode(),
                                              b",", 6, C.ptr(cst)), G.handle)
+        # two runs of the device sums differ in the last bits (fp64 atomics): the
+        # files are equal line by line up to a %.6f HALF_UP boundary decided by
+        # an ulp, and ids equal except where two scores tie within that noise
         for suf in ("", ".sim.txt"):
-            assert open(jp + suf, "rb").read() == open(cp + suf, "rb").read()
+            a = open(jp + suf, "rb").read().decode().split("\r\n")
+            b = open(cp + suf, "rb").read().decode().split("\r\n")
+            assert len(a) == len(b) == ns + 1 and a[-1] == b[-1] == ""
+            ndiff = 0
+            for la, lb in zip(a[:-1], b[:-1]):
+                if la == lb:
+                    continue
+                ta, tb = la.split(","), lb.split(",")
+                assert ta[0] == tb[0] and len(ta) == len(tb)
+                for x, y in zip(ta[1:], tb[1:]):
+                    if x != y:
+                        ndiff += 1
+                        if ":" in x:  # the .sim.txt file: id:score
+                            (ia, va), (ib, vb) = x.split(":"), y.split(":")
+                            assert abs(float(va) - float(vb)) <= 1.000001e-6, (x, y)
+            assert ndiff <= max(2, ns * topk // 1000), ndiff
         assert np.array_equal(O.np(st, I64, 4), cst)
         # top-k
         k = 50
@@ -256,8 +277,10 @@ def test_jni_gpu_driver_sequence_equals_c_abi(jni, gw, tmp_path):
         ci, cs, cst = np.zeros(ns * k, np.int32), np.zeros(ns * k), np.zeros(4, np.int64)
         C.check(C.lib().gw_topsim_host(G.handle, 0, sample, step, 0.6, seed, C.ptr(src), ns, k, C.ptr(ci), C.ptr(cs),
                                        None, C.ptr(cst)), G.handle)
-        assert np.array_equal(O.np(ids_o, I32, ns * k), ci)
-        np.testing.assert_allclose(O.np(sc_o, F64, ns * k), cs, rtol=1e-12)
+        gi, gs = O.np(ids_o, I32, ns * k), O.np(sc_o, F64, ns * k)
+        np.testing.assert_allclose(gs, cs, rtol=1e-12)
+        swap = gi != ci  # ids equal except where two scores tie within fp64 atomic-order noise
+        assert np.all(np.abs(cs[swap] - gs[swap]) <= 1e-12 * np.abs(cs[swap]))
         assert np.array_equal(O.np(st_o, I64, 4)[[0, 1, 3]], cst[[0, 1, 3]])
         # dense rows
         rows, rs = O.rows(ns, 1380)
