@@ -1214,13 +1214,19 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
     };
     // this thread's LDS-table slots -> the candidate list (touched / ov_list
     // from s_novc on), cleared; keys placed by a wave scan + one LDS atomic
-    auto dump_lds = [&]() {
+    // (entries whose key is below tl cannot reach the source's top k: dropped)
+    auto dump_lds = [&](unsigned long long tl) {
       constexpr int SPT_D = HASH_SLOTS / BLOCK;
       int32_t kk[SPT_D];
       int mine = 0;
 #pragma unroll
       for (int i = 0; i < SPT_D; ++i) {
         kk[i] = s_hkey[tid + i * BLOCK];
+        if (kk[i] != -1 && tl != 0ull && dkey(s_hval[tid + i * BLOCK]) < tl) {
+          s_hkey[tid + i * BLOCK] = -1;  // below the bound: cleared, not listed
+          s_hval[tid + i * BLOCK] = 0.0;
+          kk[i] = -1;
+        }
         mine += kk[i] != -1;
       }
       // (lane made opaque: its compare masks are not hoisted into scalar
@@ -1275,6 +1281,15 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       int32_t* cl = claim_base();
       const int cap34 = (int)(A.touch_cap * 3 / 4);
       mark(13);
+      // top-k rows only: a lower bound on the source's K-th largest score from
+      // the final values of the LDS table (every key left there is final:
+      // its other updates were folded in below), by two radix passes over
+      // its slots — the key's bin lower edge with >= K table entries at or
+      // above it.  Partition and HBM candidates below it cannot make the top
+      // k and are never listed (the list was ~36k entries per stretch source,
+      // re-read by every selection pass).
+      const bool prune = A.out_ids && !A.out_rows && !A.sp.cursor && A.topk > 0 && !(kGwDiag && (A.diag & 65536));
+      unsigned long long tlb = 0ull;
       // (0) claimed HBM keys held by the LDS table (a folded entry keeps its key
       // for the probe chains; value 0 marks it: pair updates are > 0)
       int nt = min(s_ntouch, cap34);
@@ -1285,8 +1300,50 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         fold_lds(key, v, fold_cap);
         if (v == 0.0) __hip_atomic_store(&ov_val[2 * slot + 1], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (prune) {
+        for (int b = tid; b < 256; b += BLOCK) {
+          s_hist[b] = 0;
+          s_hist2[b] = 0;
+        }
+        if (tid == 0) {
+          s_prefix = 0;
+          s_mask = 0;
+          s_need = A.topk;
+          s_all = 0;
+        }
+      }
       __syncthreads();
-      dump_lds();
+      if (prune) {
+        for (int pass = 0; pass < 2; ++pass) {
+          const int shift = 56 - 8 * pass;
+          unsigned* const Hh = pass ? s_hist2 : s_hist;
+          const unsigned long long pre = s_prefix, msk = s_mask;
+#pragma unroll
+          for (int i = 0; i < HASH_SLOTS / BLOCK; ++i)
+            if (s_hkey[tid + i * BLOCK] != -1) {
+              const unsigned long long k = dkey(s_hval[tid + i * BLOCK]);
+              if ((k & msk) == pre) atomicAdd(&Hh[(k >> shift) & 255], 1u);
+            }
+          __syncthreads();
+          if (tid < 64) {
+            int bin, before, tot;
+            select_bin_w(Hh, s_need, true, bin, before, tot);
+            if (tid == 0) {
+              if (pass == 0 && tot < A.topk) {
+                s_all = 1;  // fewer than K table entries: no bound
+              } else {
+                s_need -= before;
+                s_prefix = pre | ((unsigned long long)bin << shift);
+                s_mask = msk | (255ull << shift);
+              }
+            }
+          }
+          __syncthreads();
+          if (s_all) break;
+        }
+        tlb = s_all ? 0ull : (unsigned long long)s_prefix;
+      }
+      dump_lds(tlb);
       __syncthreads();
       mark(10);  // diagnostics: claims folded into the table + table dump
       for (int p = 0; p < NP; ++p) {  // (1)
@@ -1320,7 +1377,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           }
           __syncthreads();
         }
-        dump_lds();
+        dump_lds(tlb);
         __syncthreads();
       }
       mark(11);  // diagnostics: partition reduces
@@ -1339,7 +1396,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           __hip_atomic_store(&ov_key[4 * slot], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&ov_val[2 * slot + 1], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        const bool keep = v != 0.0;
+        const bool keep = v != 0.0 && dkey(v) >= tlb;
         const unsigned long long m = __ballot(keep);
         int wbase = 0;
         if (lane == 0 && m) wbase = atomicAdd(&s_novc, __popcll(m));
