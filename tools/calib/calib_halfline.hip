@@ -20,7 +20,7 @@
 // The dword's value enters the next address, so it is a dependent read.
 //
 //   calib_halfline [--sizes MB,..] [--modes 0,1,2,3] [--waves 5] [--iters N]
-// Prints one JSON object per line; tools/gpu_halfline.sh adds rocprofv3
+// Prints one JSON object per line; round 2 ran it with tools/gpu_halfline.sh (now `tools/gpu_run.sh py` / `counters`), which added rocprofv3
 // TCC_EA0_RDREQ / TCC_HIT / TCC_MISS passes (requests per walker-iteration).
 #include <hip/hip_runtime.h>
 #include <stdio.h>

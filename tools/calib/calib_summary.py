@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a tools/gpu_calib.sh run into profiles/calib_<tag>.json.
+"""Summarise a `tools/gpu_run.sh calib` run (rounds 1-4: tools/gpu_calib.sh) into profiles/calib_<tag>.json.
 
 The PMC runs launch, per (table size, read size), one warm-up and one timed
 dispatch of k_coop<RB,1> in the order the sweep prints its lines; rocprofv3's
@@ -34,7 +34,7 @@ def pmc(dirp):
 def main():
     src, tag = sys.argv[1], sys.argv[2]
     sweep = load_jsonl(os.path.join(src, "sweep.jsonl"))
-    out = {"tool": "tools/calib/calib_sweep.hip via tools/gpu_calib.sh", "tag": tag,
+    out = {"tool": "tools/calib/calib_sweep.hip via tools/gpu_run.sh calib", "tag": tag,
            "definition": "random RB-byte blocks (RB-aligned), read cooperatively (RB/16 lanes per block), "
                          "DEP=1: next address depends on the data read; W waves per SIMD forced by LDS",
            "sweep": sweep, "pmc": []}

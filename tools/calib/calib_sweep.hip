@@ -18,7 +18,7 @@
 //
 // Output: one JSON object per line:
 //   {"rb":64,"dep":0,"waves":5,"table_mb":2048,"blocks_per_s":..,"bytes_per_s":..,"ms":..,"reads":..}
-// tools/gpu_calib.sh runs the sweep plus rocprofv3 TCC_EA0_RDREQ passes and
+// tools/gpu_run.sh calib (rounds 1-4: tools/gpu_calib.sh) runs the sweep plus rocprofv3 TCC_EA0_RDREQ passes and
 // writes profiles/calib_<tag>.json (bench.py reads the rate from there).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
