@@ -734,27 +734,67 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       if (!cf_insert(target, val)) ov_add(target, val);
       return;
     }
-    for (int probe = 0; probe < HASH_SLOTS; ++probe) {
-      const int32_t k = s_hkey[h];
-      if (k == target) {
-        atomicAdd(&s_hval[h], val);
-        return;
+    if (PIPE) {
+      // the same probe, four keys per ds_read_b128: once the table is full
+      // (every heavy source's walk) an unsuccessful search runs to the end of
+      // its cluster — ~8.5 slots on average at 75% load and several times
+      // that for the slowest lane of a wave, which the whole wave waits for.
+      // Stretch -3.9%, P10M -1.1%; the unpipelined kernel (arxiv, SAMPLE >=
+      // 2500) +4%: not there (profiles/r06/tsab_r06n.jsonl, tsab_r06o.jsonl)
+      for (int probed = 0; probed < HASH_SLOTS;) {
+        const uint32_t g0 = h & ~3u;
+        const int4 kv = *reinterpret_cast<const int4*>(&s_hkey[g0]);
+        const int32_t ks[4] = {kv.x, kv.y, kv.z, kv.w};
+        int at = 4;  // the first slot at or after h holding the key or empty
+        bool hit = false;
+#pragma unroll
+        for (int j = 3; j >= 0; --j)
+          if ((uint32_t)j >= (h & 3u) && (ks[j] == target || ks[j] == -1)) {
+            at = j;
+            hit = ks[j] == target;
+          }
+        if (at < 4) {
+          h = g0 + (uint32_t)at;
+          if (hit) {
+            atomicAdd(&s_hval[h], val);
+            return;
+          }
+          // (APPEND: a full table is seen without the atomic — every
+          // overflowing key would otherwise take a returning atomic on this
+          // one LDS address)
+          if ((APPEND && s_hcount >= HASH_LIMIT) || atomicAdd(&s_hcount, 1) >= HASH_LIMIT) break;
+          const int32_t old = atomicCAS(&s_hkey[h], -1, target);
+          const bool mine = old == -1 || old == target;
+          if (APPEND) atomicAdd(&s_hdone, 1);  // (after the CAS has returned)
+          if (mine) {
+            atomicAdd(&s_hval[h], val);
+            return;
+          }
+          h = H::next(h);  // another key took the slot: go on after it
+          ++probed;
+          continue;
+        }
+        probed += 4 - (int)(h & 3u);
+        h = g0 + 4u == (uint32_t)HASH_SLOTS ? 0u : g0 + 4u;
       }
-      if (k == -1) {
-        // reserve an LDS entry first; past the load limit new keys overflow
-        // (APPEND: a full table is seen without the atomic — every
-        // overflowing key would otherwise take a returning atomic on this
-        // one LDS address)
-        if ((APPEND && s_hcount >= HASH_LIMIT) || atomicAdd(&s_hcount, 1) >= HASH_LIMIT) break;
-        const int32_t old = atomicCAS(&s_hkey[h], -1, target);
-        const bool mine = old == -1 || old == target;
-        if (APPEND) atomicAdd(&s_hdone, 1);  // (after the CAS has returned)
-        if (mine) {
+    } else {
+      for (int probe = 0; probe < HASH_SLOTS; ++probe) {
+        const int32_t k = s_hkey[h];
+        if (k == target) {
           atomicAdd(&s_hval[h], val);
           return;
         }
+        if (k == -1) {
+          // reserve an LDS entry first; past the load limit new keys overflow
+          if (atomicAdd(&s_hcount, 1) >= HASH_LIMIT) break;
+          const int32_t old = atomicCAS(&s_hkey[h], -1, target);
+          if (old == -1 || old == target) {
+            atomicAdd(&s_hval[h], val);
+            return;
+          }
+        }
+        h = H::next(h);
       }
-      h = H::next(h);
     }
     if (APPEND && s_heavy && s_hdone >= HASH_LIMIT) {
       // append-and-reduce source whose LDS table is final (every reserved

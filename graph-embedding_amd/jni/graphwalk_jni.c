@@ -2,8 +2,10 @@
  * drivers, e.g. Test_u_u_TopSim_singleSample.java:46-64) calling libgraphwalk's
  * C ABI (include/graphwalk.h).  Java class: simrank.GraphWalkNative.
  *
- * UNTESTED HERE: this image has no JDK (no jni.h, no javac), so build.py
- * compiles this file only when $JAVA_HOME/include/jni.h exists:
+ * This image has no JDK (no jni.h, no javac): tests/test_jni_shim.py compiles
+ * this file -Wall -Wextra -Werror against a test-only <jni.h> stand-in and
+ * drives every entry point through a fake JNIEnv (no JVM).  build.py builds
+ * the real shim only when $JAVA_HOME/include/jni.h exists:
  *   cc -shared -fPIC -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -Iinclude \
  *      graph-embedding_amd/jni/graphwalk_jni.c -Lgraph-embedding_amd/gwamd -lgraphwalk \
  *      -o graph-embedding_amd/gwamd/libgraphwalk_jni.so

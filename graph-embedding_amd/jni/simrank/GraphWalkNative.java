@@ -4,7 +4,8 @@ package simrank;
  * Native bindings of libgraphwalk (include/graphwalk.h) through
  * graph-embedding_amd/jni/graphwalk_jni.c.
  *
- * UNTESTED HERE: the build image has no JDK; build.py compiles the shim only
+ * No JVM in the build image: the C shim is compiled and driven through a fake
+ * JNIEnv by tests/test_jni_shim.py; build.py compiles the real shim only
  * when $JAVA_HOME/include/jni.h exists.  Load order: libgraphwalk.so, then
  * libgraphwalk_jni.so (java.library.path = graph-embedding_amd/gwamd).
  */

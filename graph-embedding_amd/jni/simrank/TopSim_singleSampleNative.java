@@ -10,7 +10,8 @@ import conf.MyConfiguration;
  * Philox-keyed by (seed, source, walker, level) instead of the reference's
  * unseeded static java.util.Random (Graph.java:17).
  *
- * UNTESTED HERE (no JDK in the build image); the C++ port of the same driver
+ * Not compiled here (no JDK in the build image; the native methods it calls are
+ * exercised through a fake JNIEnv by tests/test_jni_shim.py); the C++ port of the same driver
  * (graph-embedding_amd/host/) runs in the GPU tests.
  */
 public class TopSim_singleSampleNative {
