@@ -269,11 +269,12 @@ int gw_graph_free(gw_graph* g) {
 int gw_graph_set_options(gw_graph* g, const gw_options_t* opt) {
   if (!g) return gw_fail(nullptr, GW_ERR_INVALID, "NULL handle");
   if (!opt) {
-    g->opt = gw_options_t{0, 0, -1, 0, 0};
+    g->opt = gw_options_t{0, 0, -1, 0, 0, 0, 0};
     return GW_OK;
   }
   if (opt->table_budget_bytes < 0 || opt->expected_steps < 0 || opt->listed < -1 || opt->listed > 1 ||
-      opt->simrank_hbm_row < 0 || opt->simrank_hbm_row > 1 || opt->host_chunk_bytes < 0)
+      opt->simrank_hbm_row < 0 || opt->simrank_hbm_row > 1 || opt->host_chunk_bytes < 0 ||
+      opt->topsim_part_shrink < 0 || opt->topsim_part_shrink > 8 || opt->reserved0 != 0)
     return gw_fail(g, GW_ERR_INVALID, "option out of range");
   g->opt = *opt;
   return GW_OK;

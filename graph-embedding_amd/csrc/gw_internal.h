@@ -148,7 +148,7 @@ struct gw_ts_sparse {
 };
 
 struct gw_graph {
-  gw_options_t opt{0, 0, -1, 0, 0};  // per-handle tuning (gw_graph_set_options)
+  gw_options_t opt{0, 0, -1, 0, 0, 0, 0};  // per-handle tuning (gw_graph_set_options)
   // host CSR
   int semantics = 0;
   int directed = 0;

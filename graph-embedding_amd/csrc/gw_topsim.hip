@@ -92,7 +92,7 @@ struct TsArgs {
   int64_t heavy_min;   // a source appends past the LDS table when its pair-update bound exceeds this
   int32_t* claim;      // [blocks][touch_cap] a heavy source's claimed overflow-hash slots
   int part_entries;    // a heavy source gets the power of two of partitions that keeps its bound <= this each
-  int pcap_shrink;     // -DGW_DIAG only (GW_DIAG_TS_PCAP_SHRINK): partitions 2^-k of their room, to force flag 8
+  int pcap_shrink;     // gw_options_t.topsim_part_shrink: partitions get 2^-k of their room (tests flag 8's re-run)
   unsigned int* src_counter;
   int* error_flag;
   unsigned long long* phase;  // diagnostics (GW_DIAG_TS_PHASES): cycles per phase, thread 0 of each block
@@ -1014,7 +1014,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         if (!LDS_ROW) s_ovmask = s_pm[cur].ovmask;
         s_heavy = (APPEND && !LDS_ROW) ? s_pm[cur].heavy : 0;
         s_plg = s_pm[cur].plg;
-        s_pinfo = s_plg | ((31 - __builtin_clz((uint32_t)A.touch_cap) - s_plg - (kGwDiag ? A.pcap_shrink : 0)) << 8);
+        s_pinfo = s_plg | ((31 - __builtin_clz((uint32_t)A.touch_cap) - s_plg - A.pcap_shrink) << 8);
       }
       __syncthreads();
     } else {
@@ -2346,8 +2346,8 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   A.part_entries = 3584;  // ~ the distinct keys one 6144-slot LDS fill takes comfortably
   if (const char* pe = GW_DIAG_ENV("GW_DIAG_TS_PART"))  // A/B knob: partition size bound
     A.part_entries = std::max(256, std::atoi(pe));
-  A.pcap_shrink = 0;
-  if (const char* pc = GW_DIAG_ENV("GW_DIAG_TS_PCAP_SHRINK"))  // test knob: partitions overflow -> re-run (flag 8)
+  A.pcap_shrink = g->opt.topsim_part_shrink;  // (tests: partitions overflow -> re-run, flag 8)
+  if (const char* pc = GW_DIAG_ENV("GW_DIAG_TS_PCAP_SHRINK"))
     A.pcap_shrink = std::min(8, std::max(0, std::atoi(pc)));
   A.heavy_min = 2 * (int64_t)(t.lds_row == 1 ? TsHash<1>::LIMIT : TsHash<2>::LIMIT);
   A.src_counter = t.src_counter;

@@ -80,7 +80,8 @@ class Options(ctypes.Structure):
     """gw_options_t (per-handle tuning, include/graphwalk.h)."""
     _fields_ = [("table_budget_bytes", ctypes.c_int64), ("expected_steps", ctypes.c_int64),
                 ("listed", ctypes.c_int32), ("simrank_hbm_row", ctypes.c_int32),
-                ("host_chunk_bytes", ctypes.c_int64)]
+                ("host_chunk_bytes", ctypes.c_int64), ("topsim_part_shrink", ctypes.c_int32),
+                ("reserved0", ctypes.c_int32)]
 
 
 P = ctypes.c_void_p

@@ -142,6 +142,12 @@ typedef struct gw_options_t {
   int32_t simrank_hbm_row;
   /* gw_n2v_walks_host staging chunk in bytes; 0 = 256 MB                   */
   int64_t host_chunk_bytes;
+  /* TopSim (pipelined kernel, STEP >= 4): a heavy source's key-hash
+   * partitions get 2^-k of their room (0..8; 0 = all).  A partition that
+   * fills makes the call re-run without the append path (same scores);
+   * exists to test that fallback                                          */
+  int32_t topsim_part_shrink;
+  int32_t reserved0;  /* 0 */
 } gw_options_t;
 
 typedef struct gw_topsim_stats_t {

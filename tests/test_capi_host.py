@@ -378,11 +378,14 @@ def test_options_roundtrip_and_validation(gw):
     from gwamd import _lib as C
     G = gw.GWGraph.from_edgelist(os.path.join(DATA, "karate.edgelist"), " ", "nx")
     d = G.options()
-    assert d == dict(table_budget_bytes=0, expected_steps=0, listed=-1, simrank_hbm_row=0, host_chunk_bytes=0)
-    d = G.options(expected_steps=123, listed=0, host_chunk_bytes=1 << 20)
+    assert d == dict(table_budget_bytes=0, expected_steps=0, listed=-1, simrank_hbm_row=0, host_chunk_bytes=0,
+                     topsim_part_shrink=0, reserved0=0)
+    d = G.options(expected_steps=123, listed=0, host_chunk_bytes=1 << 20, topsim_part_shrink=3)
     assert d["expected_steps"] == 123 and d["listed"] == 0 and d["host_chunk_bytes"] == 1 << 20
-    bad = C.Options(0, 0, 2, 0, 0)
-    assert C.lib().gw_graph_set_options(G.handle, ctypes.byref(bad)) == C.GW_ERR_INVALID
+    assert d["topsim_part_shrink"] == 3
+    for bad in (C.Options(0, 0, 2, 0, 0, 0, 0), C.Options(0, 0, 0, 0, 0, 9, 0), C.Options(0, 0, 0, 0, 0, -1, 0),
+                C.Options(0, 0, 0, 0, 0, 0, 1)):
+        assert C.lib().gw_graph_set_options(G.handle, ctypes.byref(bad)) == C.GW_ERR_INVALID
     assert C.lib().gw_graph_set_options(G.handle, None) == 0
     assert G.options()["listed"] == -1
 

@@ -357,6 +357,56 @@ def test_topsim_stretch_heavy_sources_sparse_and_dense_rows(gw, oracle):
     assert int(st2[1]) == rst["pair_updates"]
 
 
+def test_topsim_partition_overflow_reruns_without_append(gw, oracle):
+    """The append path's fallback: with gw_options_t.topsim_part_shrink = 5 a
+    heavy source's key-hash partitions get 1/32 of their room, so they fill
+    (flag 8) and gw_dev_topsim re-runs the launch without the append path,
+    from the caller's counters and sparse-row cursor as they were.  Top-k
+    rows, sparse rows and exact counters against the oracle (1M-vertex Java
+    R-MAT, SAMPLE 10000 / STEP 5, hubs + strided sources)."""
+    import torch
+    from gwamd import _lib as Cl
+    g = gw.GWGraph.rmat_java(1_000_000, 10_000_000, 0.57, 0.19, 0.19, 42)
+    c = g.export_csr()
+    offs, nbrs = c["offsets"], c["nbrs"]
+    deg = np.diff(offs)
+    nz = np.nonzero(deg > 0)[0]
+    pick = np.concatenate([nz[np.argsort(deg[nz])[-2:]], nz[np.linspace(0, len(nz) - 1, 14).astype(np.int64)]])
+    pick = pick.astype(np.int32)
+    g.to_device(0)
+    assert g.options(topsim_part_shrink=5)["topsim_part_shrink"] == 5
+    K, sample, step = 100, 10000, 5
+    src = torch.as_tensor(pick, device="cuda")
+    ids = torch.empty((len(pick), K), dtype=torch.int32, device="cuda")
+    sc = torch.empty((len(pick), K), dtype=torch.float64, device="cuda")
+    st = torch.full((4,), 7, dtype=torch.int64, device="cuda")  # accumulated onto, as the caller's counters
+    Cl.check(Cl.lib().gw_topsim(g.handle, 0, sample, step, 0.6, 42, Cl.ptr(src), len(pick), K, Cl.ptr(ids),
+                                Cl.ptr(sc), Cl.ptr(st), None), g.handle)
+    oi, osc, ost = oracle.topsim_topk(offs, nbrs, 0, sample, step, K, C=0.6, seed=42, sources=pick, nthreads=8)
+    stg = st.cpu().numpy()
+    assert int(stg[0]) == 7 + ost["extensions"] and int(stg[1]) == 7 + ost["pair_updates"]
+    assert int(stg[3]) == 7 + ost["walkers"]
+    _topk_match(ids.cpu().numpy(), sc.cpu().numpy(), oi, osc)
+    # sparse rows through the re-run: the cursor restarts where the caller left it
+    ref, rst = oracle.topsim(offs, nbrs, 0, sample, step, C=0.6, seed=42, sources=pick[:4], nthreads=8)
+    cap = 400_000
+    b = torch.empty(4, dtype=torch.int64, device="cuda")
+    ln = torch.empty(4, dtype=torch.int32, device="cuda")
+    sid = torch.empty(cap, dtype=torch.int32, device="cuda")
+    ssc = torch.empty(cap, dtype=torch.float64, device="cuda")
+    used = torch.zeros(1, dtype=torch.int64, device="cuda")
+    st2 = torch.zeros(4, dtype=torch.int64, device="cuda")
+    Cl.check(Cl.lib().gw_topsim_sparse(g.handle, 0, sample, step, 0.6, 42, Cl.ptr(src), 4, cap, Cl.ptr(b), Cl.ptr(ln),
+                                       Cl.ptr(sid), Cl.ptr(ssc), Cl.ptr(used), Cl.ptr(st2), None), g.handle)
+    B, LN, I, S = b.cpu().numpy(), ln.cpu().numpy(), sid.cpu().numpy(), ssc.cpu().numpy()
+    assert int(used.cpu()[0]) == int(LN.sum()) and int(st2[1]) == rst["pair_updates"]
+    for r in range(4):
+        row_ids = I[B[r]:B[r] + LN[r]]
+        assert np.array_equal(np.sort(row_ids), np.nonzero(ref[r])[0])
+        np.testing.assert_allclose(S[B[r]:B[r] + LN[r]], ref[r][row_ids], rtol=1e-12, atol=0)
+    g.options(topsim_part_shrink=0)
+
+
 def test_mirror_compute_and_print(gw, oracle, tmp_path):
     """TopSim_singleSample mirror + printByOrder on GPU dense rows == Java
     emulation over the oracle rows."""
