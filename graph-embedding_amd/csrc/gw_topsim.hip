@@ -631,6 +631,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
   const bool enumerate_all = !PIPE && (A.variant == GW_TOPSIM_ENUMERATE);
 
   long long my_ext = 0, my_upd = 0, my_walk = 0, my_maxf = 0;
+  unsigned long long w1_t = 0, w1_walk = 0, w1_wait = 0;  // diagnostics: wave 1's walker phase
   // deferred ordering of the top-k rows (the dense / sparse row writers keep the in-place phase)
   const bool defer = DEFER && A.out_ids && !(kGwDiag && (A.diag & 32));
   int64_t pend_r = -1;  // the source whose selected entries await ranking
@@ -1195,6 +1196,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       const double* EVb = A.enum_val + (blk * 2 + cur) * A.enum_cap;
       int32_t pt = -1;
       double pv = 0.0;
+      if (kGwDiag && A.phase && tid == 64) w1_t = __builtin_readcyclecounter();
       for (;;) {
         unsigned base = 0u;
         if (lane == 0) base = atomicAdd(&s_wnext, 64u);
@@ -1207,6 +1209,11 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           add(ETb[g - p_nw], EVb[g - p_nw]);
       }
       if (pt >= 0) add(pt, pv);
+      if (kGwDiag && A.phase && tid == 64) {  // diagnostics: a walker wave's walk / wait at the barrier
+        const unsigned long long now = __builtin_readcyclecounter();
+        w1_walk += now - w1_t;
+        w1_t = now;
+      }
     } else {
       const int W = s_nwalk;
       const int ns = s_nspawn;
@@ -1216,6 +1223,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
       if (pt >= 0) add(pt, pv);
     }
     __syncthreads();
+    if (PIPE && kGwDiag && A.phase && tid == 64) w1_wait += __builtin_readcyclecounter() - w1_t;
 
     mark(2);
     // ---- output ------------------------------------------------------------
@@ -1922,6 +1930,10 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
 
   if (kGwDiag && A.phase && tid == 0)
     for (int k = 0; k < 15; ++k) atomicAdd(&A.phase[k], s_ph[k]);
+  if (kGwDiag && A.phase && tid == 64) {
+    atomicAdd(&A.phase[15], w1_walk);
+    atomicAdd(&A.phase[16], w1_wait);
+  }
   // statistics
   long long e = block_sum<long long, NW>(my_ext, s_red);
   long long u = block_sum<long long, NW>(my_upd, s_red);
@@ -2359,8 +2371,8 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
   const char* dph = GW_DIAG_ENV("GW_DIAG_TS_PHASES");
   A.phase = nullptr;
   if (dph && dph[0] == '1') {
-    GW_HIP_TRY(hipMalloc((void**)&A.phase, 15 * sizeof(unsigned long long)));
-    GW_HIP_TRY(hipMemsetAsync(A.phase, 0, 15 * sizeof(unsigned long long), s));
+    GW_HIP_TRY(hipMalloc((void**)&A.phase, 17 * sizeof(unsigned long long)));
+    GW_HIP_TRY(hipMemsetAsync(A.phase, 0, 17 * sizeof(unsigned long long), s));
   }
   // a heavy source's key-hash partition can overflow only when one key that
   // missed the LDS table takes thousands of its pair updates (flag 8): the
@@ -2388,15 +2400,16 @@ int gw_dev_topsim(gw_graph* g, int variant, int sample, int step, double C, uint
     GW_HIP_TRY(hipMemsetAsync(t.error_flag, 0, sizeof(int), s));
   }
   if (A.phase) {
-    unsigned long long ph[15];
+    unsigned long long ph[17];
     GW_HIP_TRY(hipMemcpy(ph, A.phase, sizeof ph, hipMemcpyDeviceToHost));
     (void)hipFree(A.phase);
     const unsigned long long app = ph[10] + ph[11] + ph[12] + ph[13];
     std::fprintf(stderr, "[k_topsim phases, cycles summed over %d blocks] levels %llu walkers %llu output %llu "
                  "(count %llu radix %llu ties %llu collect %llu order %llu) clear %llu (spawn-prefix %llu) "
-                 "[count: append-reduce %llu = fold %llu scatter+dump %llu partitions %llu pre %llu]\n",
+                 "[count: append-reduce %llu = fold %llu scatter+dump %llu partitions %llu pre %llu] "
+                 "[wave 1: walking %llu, waiting at the walker barrier %llu]\n",
                  blocks, ph[0] + 0ull, ph[2], ph[3] + ph[5] + ph[6] + ph[7] + ph[8] + ph[9] + app, ph[5] + app, ph[6],
-                 ph[7], ph[8], ph[9], ph[4], ph[1], app, ph[10], ph[11], ph[12], ph[13]);
+                 ph[7], ph[8], ph[9], ph[4], ph[1], app, ph[10], ph[11], ph[12], ph[13], ph[15], ph[16]);
   }
   if (flag & 3) {
     g->err = "TopSim frontier exceeded the workspace (level/spawn/touch capacity)";
