@@ -40,7 +40,10 @@ def _oracle(oracle, g, variant, sample, step, sources, seed=11, C=0.6):
 
 
 @pytest.mark.parametrize("name,sample,step", [("moreno", 1000, 5), ("moreno", 10000, 5), ("g333", 2500, 3),
-                                              ("blog", 1000, 5), ("moreno", 40000, 2), ("g333", 100, 8)])
+                                              ("blog", 1000, 5), ("moreno", 40000, 2), ("g333", 100, 8),
+                                              # the reference driver's largest SAMPLE at its STEP
+                                              # (Test_u_u_TopSim_singleSample.java:36-38; bench config-3 sweep)
+                                              ("moreno", 40000, 5), ("blog", 40000, 5)])
 def test_topsim_dense_equals_oracle(gw, oracle, name, sample, step):
     g = _graph(gw, name)
     n = g.getVCount()
