@@ -559,7 +559,11 @@ def test_sparse_rows_equal_oracle_and_write_exact(gw, oracle, tmp_path, name, sa
 
 
 @pytest.mark.parametrize("name,sample,step,topk", [("moreno", 1000, 5, 20), ("blog", 1000, 3, 100),
-                                                   ("arxiv", 2500, 5, 20)])
+                                                   ("arxiv", 2500, 5, 20),
+                                                   # the reference driver's largest SAMPLE, its STEP and
+                                                   # topK (Test_u_u_TopSim_singleSample.java:36-38, testTopK)
+                                                   ("moreno", 40000, 5, 20), ("blog", 40000, 5, 20),
+                                                   ("arxiv", 40000, 5, 20)])
 def test_write_text_matches_java_print_on_oracle_rows(gw, oracle, tmp_path, name, sample, step, topk):
     """gw_topsim_write_text (compute + Print.printByOrder at any V, the path
     of config 5 and the JNI writer) against Print.printByOrder's Java
