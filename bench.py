@@ -1487,9 +1487,45 @@ def main(argv):
             res["reference_cpu_context"] = {"file": "profiles/cpu_reference_node2vec.json",
                                             "summary": ref.get("summary")}
         res["secondary"] = secondary or None
+        res["summary"] = tail_summary(res)
         print(json.dumps(res), flush=True)
     R.close()
     return 0
+
+
+def tail_summary(res):
+    """A compact digest of the secondary lines, printed LAST in the JSON line:
+    a driver that keeps only the line's tail (the last ~2000 characters) still
+    records every config-3 point and the config-5 lines.  Lists, no key names:
+    config3 rows are [graph, SAMPLE, kernel ms, pair-updates/s, roofline frac,
+    counter traffic GB (null: no keyed PMC entry), kernel, scratch B/lane]."""
+    sec = res.get("secondary") or {}
+
+    def r3(x):
+        return None if x is None else float(f"{x:.3g}")
+
+    def e3(x):  # large rates as short strings ("3.59e+10")
+        return None if x is None else f"{x:.3g}"
+    out = {}
+    pts = (sec.get("topsim_config3") or {}).get("points") or []
+    if pts:
+        out["config3_cols"] = "graph,SAMPLE,ms,pair-updates/s,frac,traffic_GB,kernel,scratch_B"
+        out["config3"] = [[p["graph"], p["sample"], round(p["seconds"] * 1e3, 2), e3(p["value"]),
+                           round(p["roofline"]["frac"], 3),
+                           None if p["roofline"].get("traffic") is None else round(p["roofline"]["traffic"] / 1e9, 1),
+                           (p.get("kernel") or "").replace("k_topsim_", "").replace(" ", "").replace("<", "")
+                           .replace(">", ""),
+                           (p.get("kernel_attrs") or {}).get("scratch_bytes_per_lane")] for p in pts]
+    for k in ("topsim_p10m", "topsim_p10m_stretch", "walk_rmat24_p1q05"):
+        v = sec.get(k)
+        if not v or not v.get("roofline"):
+            continue
+        r = v["roofline"]
+        out[k] = {"s": r3(v.get("seconds") or (v.get("kernel_ms") or 0) * 1e-3), "value": e3(v.get("value")),
+                  "frac": r3(r.get("frac")), "traffic_GB": None if r.get("traffic") is None else round(r["traffic"] / 1e9, 1),
+                  "rate": r3((r.get("random_line_roofline") or {}).get("frac")),
+                  "host_shard_s": r3((v.get("host_shard") or {}).get("seconds"))}
+    return out or None
 
 
 def gwamd_graph_rmat(scale, ef, a, b, c, seed):
