@@ -766,7 +766,7 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
           if ((APPEND && s_hcount >= HASH_LIMIT) || atomicAdd(&s_hcount, 1) >= HASH_LIMIT) break;
           const int32_t old = atomicCAS(&s_hkey[h], -1, target);
           const bool mine = old == -1 || old == target;
-          if (APPEND) atomicAdd(&s_hdone, 1);  // (after the CAS has returned)
+          if (APPEND) atomicAdd(&s_hdone, 1);  // (after the CAS has returned: device ISA checked)
           if (mine) {
             atomicAdd(&s_hval[h], val);
             return;
@@ -797,6 +797,10 @@ __device__ __forceinline__ void topsim_body(const TsArgs& A) {
         h = H::next(h);
       }
     }
+    // (order: a lane's count follows its CAS — the compiler waits for the CAS
+    // before issuing the add — and the slot re-read below is control-dependent
+    // on this check; both checked in the gfx950 assembly.  Explicit fences or
+    // compiler barriers here cost 16 B more scratch per lane.)
     if (APPEND && s_heavy && s_hdone >= HASH_LIMIT) {
       // append-and-reduce source whose LDS table is final (every reserved
       // insert has landed).  Slots never empty and keys never change, so the
